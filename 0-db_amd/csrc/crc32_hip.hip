@@ -1,0 +1,657 @@
+// crc32_hip.hip -- MI355X (gfx950) batched record checksum for 0-db.
+//
+// Computes out[r] = zdb_crc32(arena + offsets[r], lengths[r]) for n records
+// in one pass over HBM (libzdb/crc32.c:145-155 semantics: CRC-32C, reflected
+// 0x82F63B78, init 0, no final XOR).  Callers it serves: the SET path
+// (commands_set.c:106/:216, api.c:124/:204), CHECK (data.c:564) and the
+// integrity scan (integrity-check.c:90).
+//
+// Design (DESIGN.md §3 has the derivation and the roofline):
+//  * The checksum is GF(2)-linear with crc(0^k || X) = crc(X) (init 0, no
+//    xorout), so a record can be cut into aligned 16-byte "pieces", each
+//    piece's contribution computed independently and XORed, provided each is
+//    shifted by the number of bytes that follow it.
+//  * Work is balanced by bytes: an exclusive scan over per-record "units"
+//    (pieces + a fixed per-record charge) gives every wave of a persistent
+//    grid an equal slice of the unit space.  A wave walks the records of its
+//    slice; records cut by a slice edge are finished by atomic XOR of the
+//    partial contributions (XOR is the field addition, so the result does not
+//    depend on the order).
+//  * Inside a record segment the wave reads 1 KiB per step, fully coalesced
+//    (lane l <- bytes [16l, 16l+16) of the step), steps counted backwards
+//    from the segment end so the last piece always lands on lane 63.  Each
+//    lane keeps a 32-bit register A (Horner over its own pieces, 1 KiB apart).
+//    K = 4 steps form a superstep: slot i's tables already include the shift
+//    over the (K-1-i) KiB that follow it, so the register is advanced once per
+//    superstep.  At the end, lane l's register is shifted by 16*(63-l) bytes
+//    (lane-specific tables) and the wave XOR-reduces.
+//  * Every table maps a 5-bit slice to a 32-bit contribution.  32 dwords fill
+//    the 32 banks of a ds_read_b32 lane group exactly, so every lookup
+//    wave-instruction is bank-conflict free whatever the data; the
+//    lane-specific tables are laid out [slice][value][lane] so lane l always
+//    hits bank l.  No MFMA: this is a byte reduction.
+//  * Pieces are read at 16-byte-aligned addresses; bytes outside the record
+//    are zeroed (leading zeros are free, trailing z bytes are removed with
+//    one inverse shift x^(-8z) on the scalar unit).
+
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <mutex>
+#include <vector>
+
+#include <hip/hip_runtime.h>
+#include <rocprim/device/device_scan.hpp>
+#include <rocprim/iterator/counting_iterator.hpp>
+#include <rocprim/iterator/transform_iterator.hpp>
+
+#include "crc32c_gf2.h"
+#include "zdb_crc32.h"
+
+namespace {
+
+constexpr int K = ZDBCRC_K;
+constexpr int PCH = ZDBCRC_PCH;
+constexpr int SCH = ZDBCRC_SCH;
+constexpr int WG_THREADS = 512;
+constexpr int WAVES_PER_WG = WG_THREADS / 64;
+constexpr int WG_PER_CU = 2;              // 2 x 70 KiB of LDS tables per CU
+constexpr uint64_t UNIT_OVH = 16;         // planning charge per record, in pieces
+constexpr uint64_t MIN_UNITS_PER_WAVE = 256;
+
+static_assert(ZDBCRC_LDS_DW % 4 == 0, "LDS image must be 16-byte granular");
+static_assert(ZDBCRC_LDS_DW * 4 * WG_PER_CU <= 160 * 1024, "LDS budget");
+
+// ---------------------------------------------------------------------------
+// device helpers
+// ---------------------------------------------------------------------------
+
+__device__ __forceinline__ uint32_t word_of(const uint4 &v, int d) {
+    return d == 0 ? v.x : d == 1 ? v.y : d == 2 ? v.z : v.w;
+}
+
+// 5-bit slice c (bits [5c, 5c+5)) of a little-endian 128-bit piece.
+// c is a compile-time constant after unrolling.
+__device__ __forceinline__ uint32_t piece_slice(const uint4 &v, int c) {
+    const int s = 5 * c, d = s >> 5, sh = s & 31;
+    if (sh <= 27 || d == 3)
+        return (word_of(v, d) >> sh) & 31u;
+    return __builtin_amdgcn_alignbit(word_of(v, d + 1), word_of(v, d), sh) & 31u;
+}
+
+// contribution of one piece in slot I of a superstep
+template <int I>
+__device__ __forceinline__ uint32_t piece_contrib(const uint4 &v, const uint32_t *lds) {
+    uint32_t r = 0;
+#pragma unroll
+    for (int c = 0; c < PCH; c++)
+        r ^= lds[ZDBCRC_OFF_T + (I * PCH + c) * 32 + piece_slice(v, c)];
+    return r;
+}
+
+// register advanced over one superstep (K KiB)
+__device__ __forceinline__ uint32_t advance_superstep(uint32_t a, const uint32_t *lds) {
+    uint32_t r = 0;
+#pragma unroll
+    for (int c = 0; c < SCH; c++)
+        r ^= lds[ZDBCRC_OFF_W + c * 32 + ((a >> (5 * c)) & 31u)];
+    return r;
+}
+
+// lane l's register shifted by 16*(63-l) bytes; [c][v][lane] layout: bank = lane
+__device__ __forceinline__ uint32_t lane_place(uint32_t a, uint32_t lane, const uint32_t *lds) {
+    uint32_t r = 0;
+#pragma unroll
+    for (int c = 0; c < SCH; c++)
+        r ^= lds[ZDBCRC_OFF_L + (c * 32 + ((a >> (5 * c)) & 31u)) * 64 + lane];
+    return r;
+}
+
+// wave-uniform shift through a global [SCH][32] table (scalar loads)
+__device__ __forceinline__ uint32_t uniform_shift(uint32_t x, const uint32_t *__restrict__ tab) {
+    uint32_t r = 0;
+#pragma unroll
+    for (int c = 0; c < SCH; c++)
+        r ^= tab[c * 32 + ((x >> (5 * c)) & 31u)];
+    return r;
+}
+
+__device__ __forceinline__ uint32_t wave_xor(uint32_t x) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1)
+        x ^= __shfl_xor(x, o, 64);
+    return x;
+}
+
+// keep bytes [lo, hi) of dword k of a 16-byte piece (0 <= lo <= hi <= 16)
+__device__ __forceinline__ uint32_t keep_mask(int lo, int hi, int k) {
+    const int a = lo - 4 * k, b = hi - 4 * k;
+    const uint32_t mh = b >= 4 ? 0xFFFFFFFFu : b <= 0 ? 0u : ((1u << (8 * b)) - 1u);
+    const uint32_t ml = a <= 0 ? 0xFFFFFFFFu : a >= 4 ? 0u : (0xFFFFFFFFu << (8 * a));
+    return mh & ml;
+}
+
+__device__ __forceinline__ uint4 mask_piece(uint4 v, int lo, int hi) {
+    v.x &= keep_mask(lo, hi, 0);
+    v.y &= keep_mask(lo, hi, 1);
+    v.z &= keep_mask(lo, hi, 2);
+    v.w &= keep_mask(lo, hi, 3);
+    return v;
+}
+
+struct SegCtx {
+    uint64_t P0;      // 16-aligned address of the record's first piece
+    int64_t base_j;   // piece index of (step 0, lane 0); piece = base_j + 64 t + lane
+    uint32_t pa;      // first piece of the segment (record-relative)
+    uint32_t np;      // pieces in the record
+    int lo0;          // first record byte inside piece 0
+    int hi_last;      // one past the last record byte inside piece np-1
+};
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef const __attribute__((address_space(1))) u32x4 global_u32x4;
+
+__device__ __forceinline__ uint4 load_piece(const SegCtx &s, uint32_t t, uint32_t lane) {
+    const int64_t jj = s.base_j + 64 * (int64_t)t + (int64_t)lane;
+    u32x4 v = {0, 0, 0, 0};
+    if (jj >= (int64_t)s.pa)
+        v = *reinterpret_cast<global_u32x4 *>(s.P0 + 16u * (uint64_t)jj);
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
+
+// zero the bytes of a piece that lie outside the record (first/last piece only)
+__device__ __forceinline__ uint4 fix_edges(const SegCtx &s, uint4 v, uint32_t t, uint32_t lane) {
+    const int64_t jj = s.base_j + 64 * (int64_t)t + (int64_t)lane;
+    const bool first = jj == 0, last = jj == (int64_t)s.np - 1;
+    if (first || last)
+        v = mask_piece(v, first ? s.lo0 : 0, last ? s.hi_last : 16);
+    return v;
+}
+
+// CRC (in padded-record space) of pieces [pa, pb) of one record, wave-reduced
+__device__ __forceinline__ uint32_t segment_crc(const SegCtx &s, uint32_t pb, uint32_t lane,
+                                                const uint32_t *lds) {
+    const uint32_t nps = pb - s.pa;
+    const uint32_t T = (nps + 63u) / 64u;
+    const uint32_t S = (T + K - 1) / K;
+    const uint32_t t0 = S * K - T; // first step holding any piece of the segment
+
+    uint32_t acc = 0;
+    uint4 cur[K];
+#pragma unroll
+    for (int i = 0; i < K; i++)
+        cur[i] = load_piece(s, i, lane);
+
+    for (uint32_t ss = 0; ss < S; ss++) {
+        uint4 nxt[K];
+        const bool more = ss + 1 < S;
+        if (more) {
+#pragma unroll
+            for (int i = 0; i < K; i++)
+                nxt[i] = load_piece(s, (ss + 1) * K + i, lane);
+        }
+        if (ss)
+            acc = advance_superstep(acc, lds);
+        const uint32_t tb = ss * K;
+        if (tb + 0 >= t0) acc ^= piece_contrib<0>(fix_edges(s, cur[0], tb + 0, lane), lds);
+        if (tb + 1 >= t0) acc ^= piece_contrib<1>(fix_edges(s, cur[1], tb + 1, lane), lds);
+        if (tb + 2 >= t0) acc ^= piece_contrib<2>(fix_edges(s, cur[2], tb + 2, lane), lds);
+        if (tb + 3 >= t0) acc ^= piece_contrib<3>(fix_edges(s, cur[3], tb + 3, lane), lds);
+        if (more) {
+#pragma unroll
+            for (int i = 0; i < K; i++)
+                cur[i] = nxt[i];
+        }
+    }
+    return wave_xor(lane_place(acc, lane, lds));
+}
+
+static_assert(K == 4, "segment_crc unrolls 4 slots");
+
+__global__ __launch_bounds__(WG_THREADS, 4) void crc_batch_kernel(
+    const uint8_t *__restrict__ arena, const uint64_t *__restrict__ offsets,
+    const uint32_t *__restrict__ lengths, const uint64_t *__restrict__ unit_start, uint64_t n,
+    uint32_t *__restrict__ out, const uint32_t *__restrict__ tables, uint32_t max_waves) {
+    __shared__ __attribute__((aligned(16))) uint32_t lds[ZDBCRC_LDS_DW];
+
+    {
+        const uint4 *src = reinterpret_cast<const uint4 *>(tables);
+        uint4 *dst = reinterpret_cast<uint4 *>(lds);
+        for (int i = threadIdx.x; i < ZDBCRC_LDS_DW / 4; i += WG_THREADS)
+            dst[i] = src[i];
+    }
+    __syncthreads();
+
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t gw = __builtin_amdgcn_readfirstlane(blockIdx.x * WAVES_PER_WG + (threadIdx.x >> 6));
+    const uint64_t total = unit_start[n];
+    uint64_t nwaves = (total + MIN_UNITS_PER_WAVE - 1) / MIN_UNITS_PER_WAVE;
+    if (nwaves > max_waves)
+        nwaves = max_waves;
+    if (gw >= nwaves)
+        return;
+    const uint64_t ub = total * gw / nwaves;
+    const uint64_t ue = total * (gw + 1) / nwaves;
+    if (ub >= ue)
+        return;
+
+    // record containing unit ub: last r with unit_start[r] <= ub
+    uint64_t lo = 0, hi = n;
+    while (hi - lo > 1) {
+        const uint64_t mid = (lo + hi) >> 1;
+        if (unit_start[mid] <= ub)
+            lo = mid;
+        else
+            hi = mid;
+    }
+
+    const uint32_t *ztab = tables + ZDBCRC_OFF_Z;
+    const uint32_t *gtab = tables + ZDBCRC_OFF_G;
+
+    for (uint64_t r = lo;; r++) {
+        const uint64_t us = unit_start[r] + UNIT_OVH;
+        const uint64_t ur = unit_start[r + 1];
+        const uint64_t s_lo = ub > us ? ub : us;
+        const uint64_t s_hi = ue < ur ? ue : ur;
+        if (s_hi > s_lo) {
+            SegCtx s;
+            const uint64_t A = reinterpret_cast<uint64_t>(arena) + offsets[r];
+            const uint64_t Aend = A + lengths[r];
+            s.P0 = A & ~15ull;
+            s.np = (uint32_t)(ur - us);
+            // z zero bytes pad the record's last piece
+            const uint32_t z = (uint32_t)(s.P0 + 16u * (uint64_t)s.np - Aend);
+            s.lo0 = (int)(A & 15u);
+            s.hi_last = 16 - (int)z;
+            s.pa = (uint32_t)(s_lo - us);
+            const uint32_t pb = (uint32_t)(s_hi - us);
+            const uint32_t nps = pb - s.pa;
+            const uint32_t S = ((nps + 63u) / 64u + K - 1) / K;
+            s.base_j = (int64_t)pb - 64 * (int64_t)S * K;
+
+            uint32_t x = __builtin_amdgcn_readfirstlane(segment_crc(s, pb, lane, lds));
+
+            // remove the z zero bytes that pad the record's last piece
+            if (z)
+                x = uniform_shift(x, ztab + z * SCH * 32);
+            // shift over the record pieces that follow this segment
+            uint64_t q = s.np - pb;
+            for (int g = 0; q; g++, q >>= 1)
+                if (q & 1)
+                    x = uniform_shift(x, gtab + g * SCH * 32);
+
+            if (lane == 0) {
+                if (s.pa == 0 && pb == s.np)
+                    out[r] = x;
+                else
+                    atomicXor(&out[r], x);
+            }
+        }
+        if (ur >= ue || r + 1 >= n)
+            break;
+    }
+}
+
+// unit count per record: UNIT_OVH + number of 16-byte pieces it touches
+struct UnitCount {
+    const uint8_t *arena;
+    const uint64_t *offsets;
+    const uint32_t *lengths;
+    uint64_t n;
+    __host__ __device__ uint64_t operator()(uint64_t r) const {
+        if (r >= n)
+            return 0;
+        const uint32_t L = lengths[r];
+        if (!L)
+            return UNIT_OVH;
+        const uint64_t a = reinterpret_cast<uint64_t>(arena) + offsets[r];
+        return UNIT_OVH + (((a + L - 1) >> 4) - (a >> 4) + 1);
+    }
+};
+
+__global__ void verify_kernel(const uint32_t *__restrict__ out, const uint32_t *__restrict__ expected,
+                              uint64_t n, uint32_t *__restrict__ mismatch, uint32_t *__restrict__ count,
+                              uint32_t max_mismatch) {
+    const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r < n && out[r] != expected[r]) {
+        const uint32_t idx = atomicAdd(count, 1u);
+        if (idx < max_mismatch)
+            mismatch[idx] = (uint32_t)r;
+    }
+}
+
+__device__ __forceinline__ uint64_t mix64(uint64_t z) {
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+__global__ void synth_kernel(uint8_t *__restrict__ buf, uint64_t len, uint64_t seed) {
+    const uint64_t words = (len + 7) / 8;
+    for (uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; w < words;
+         w += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t v = mix64(seed + (w + 1) * 0x9E3779B97F4A7C15ull);
+        if (w * 8 + 8 <= len) {
+            *reinterpret_cast<uint64_t *>(buf + w * 8) = v;
+        } else {
+            for (uint64_t k = 0; w * 8 + k < len; k++)
+                buf[w * 8 + k] = (uint8_t)(v >> (8 * k));
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// host side: per-device context, workspace, launch
+// ---------------------------------------------------------------------------
+
+struct Workspace {
+    void *ptr = nullptr;
+    size_t bytes = 0;
+};
+
+struct DeviceCtx {
+    bool ready = false;
+    int cus = 0;
+    uint32_t *d_tables = nullptr;
+    std::map<void *, Workspace> ws; // per stream
+};
+
+std::mutex g_mu;
+DeviceCtx g_dev[64];
+bool g_hip_touched = false;
+bool g_timing = false;
+std::vector<std::pair<hipEvent_t, hipEvent_t>> g_pending;
+double g_time_ms = 0;
+uint64_t g_launches = 0;
+std::vector<hipEvent_t> g_event_pool;
+
+std::vector<uint32_t> &host_tables() {
+    static std::vector<uint32_t> t;
+    static std::once_flag once;
+    std::call_once(once, [] {
+        t.resize(ZDBCRC_TABLE_DW);
+        zdbcrc_build_tables(t.data());
+    });
+    return t;
+}
+
+int ensure_device(DeviceCtx **out_ctx, int *out_dev) {
+    g_hip_touched = true;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64)
+        return ZDB_CRC32_ENODEV;
+    DeviceCtx &c = g_dev[dev];
+    if (!c.ready) {
+        hipDeviceProp_t prop;
+        if (hipGetDeviceProperties(&prop, dev) != hipSuccess)
+            return ZDB_CRC32_ENODEV;
+        if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) {
+            std::fprintf(stderr, "[-] zdbcrc: device %d is %s, this build targets gfx950\n", dev,
+                         prop.gcnArchName);
+            return ZDB_CRC32_ENODEV;
+        }
+        c.cus = prop.multiProcessorCount;
+        std::vector<uint32_t> &t = host_tables();
+        if (hipMalloc(&c.d_tables, t.size() * sizeof(uint32_t)) != hipSuccess)
+            return ZDB_CRC32_ENOMEM;
+        if (hipMemcpy(c.d_tables, t.data(), t.size() * sizeof(uint32_t), hipMemcpyHostToDevice) !=
+            hipSuccess)
+            return ZDB_CRC32_ELAUNCH;
+        c.ready = true;
+    }
+    *out_ctx = &c;
+    *out_dev = dev;
+    return ZDB_CRC32_OK;
+}
+
+size_t scan_temp_bytes(uint64_t n) {
+    size_t bytes = 0;
+    auto it = rocprim::make_transform_iterator(rocprim::counting_iterator<uint64_t>(0),
+                                               UnitCount{nullptr, nullptr, nullptr, n});
+    rocprim::exclusive_scan(nullptr, bytes, it, static_cast<uint64_t *>(nullptr), uint64_t(0),
+                            n + 1, rocprim::plus<uint64_t>());
+    return bytes;
+}
+
+// enqueue memset + plan scan + main kernel; caller holds g_mu
+int enqueue_batch(DeviceCtx &c, const uint8_t *arena, const uint64_t *offsets, const uint32_t *lengths,
+                  uint32_t *out, uint64_t n, hipStream_t st) {
+    if (hipMemsetAsync(out, 0, n * sizeof(uint32_t), st) != hipSuccess)
+        return ZDB_CRC32_ELAUNCH;
+
+    const size_t us_bytes = ((n + 1) * sizeof(uint64_t) + 255) & ~size_t(255);
+    const size_t tmp_bytes = scan_temp_bytes(n);
+    const size_t need = us_bytes + tmp_bytes + 256;
+    Workspace &w = c.ws[reinterpret_cast<void *>(st)];
+    if (w.bytes < need) {
+        if (w.ptr) {
+            hipDeviceSynchronize();
+            hipFree(w.ptr);
+            w.ptr = nullptr;
+            w.bytes = 0;
+        }
+        if (hipMalloc(&w.ptr, need) != hipSuccess)
+            return ZDB_CRC32_ENOMEM;
+        w.bytes = need;
+    }
+    uint64_t *unit_start = static_cast<uint64_t *>(w.ptr);
+    void *tmp = static_cast<uint8_t *>(w.ptr) + us_bytes;
+    size_t tb = tmp_bytes;
+    auto it = rocprim::make_transform_iterator(rocprim::counting_iterator<uint64_t>(0),
+                                               UnitCount{arena, offsets, lengths, n});
+    if (rocprim::exclusive_scan(tmp, tb, it, unit_start, uint64_t(0), n + 1,
+                                rocprim::plus<uint64_t>(), st) != hipSuccess)
+        return ZDB_CRC32_ELAUNCH;
+
+    const uint32_t grid = (uint32_t)(c.cus * WG_PER_CU);
+    const uint32_t max_waves = grid * WAVES_PER_WG;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    if (g_timing) {
+        for (hipEvent_t *e : {&e0, &e1}) {
+            if (!g_event_pool.empty()) {
+                *e = g_event_pool.back();
+                g_event_pool.pop_back();
+            } else {
+                hipEventCreate(e);
+            }
+        }
+        hipEventRecord(e0, st);
+    }
+    hipLaunchKernelGGL(crc_batch_kernel, dim3(grid), dim3(WG_THREADS), 0, st, arena, offsets, lengths,
+                       unit_start, n, out, c.d_tables, max_waves);
+    if (hipGetLastError() != hipSuccess)
+        return ZDB_CRC32_ELAUNCH;
+    if (g_timing) {
+        hipEventRecord(e1, st);
+        g_pending.emplace_back(e0, e1);
+    }
+    return ZDB_CRC32_OK;
+}
+
+struct HostStaging {
+    uint8_t *arena = nullptr;
+    size_t arena_bytes = 0;
+    uint64_t *off = nullptr;
+    uint32_t *len = nullptr;
+    uint32_t *out = nullptr;
+    size_t n_cap = 0;
+    hipStream_t st = nullptr;
+};
+HostStaging g_host_staging[64];
+
+} // namespace
+
+extern "C" {
+
+const char *zdb_crc32_strerror(int code) {
+    switch (code) {
+    case ZDB_CRC32_OK: return "ok";
+    case ZDB_CRC32_ENODEV: return "no usable gfx950 HIP device";
+    case ZDB_CRC32_EINVAL: return "invalid argument";
+    case ZDB_CRC32_ENOMEM: return "device allocation failed";
+    case ZDB_CRC32_ELAUNCH: return "HIP launch/runtime error";
+    default: return "unknown error";
+    }
+}
+
+const char *zdb_crc32_batch_engine(void) {
+    std::lock_guard<std::mutex> g(g_mu);
+    for (auto &c : g_dev)
+        if (c.ready)
+            return "hip-gfx950";
+    return "uninitialized";
+}
+
+int zdb_crc32_gpu_initialized(void) { return g_hip_touched ? 1 : 0; }
+
+int zdb_crc32_batch_device(const uint8_t *d_arena, const uint64_t *d_offsets, const uint32_t *d_lengths,
+                           uint32_t *d_out, size_t n, void *stream) {
+    if (n == 0)
+        return ZDB_CRC32_OK;
+    if (!d_arena || !d_offsets || !d_lengths || !d_out)
+        return ZDB_CRC32_EINVAL;
+    std::lock_guard<std::mutex> g(g_mu);
+    DeviceCtx *c;
+    int dev;
+    int rc = ensure_device(&c, &dev);
+    if (rc)
+        return rc;
+    return enqueue_batch(*c, d_arena, d_offsets, d_lengths, d_out, n, static_cast<hipStream_t>(stream));
+}
+
+int zdb_crc32_verify_device(const uint8_t *d_arena, const uint64_t *d_offsets, const uint32_t *d_lengths,
+                            const uint32_t *d_expected, uint32_t *d_out, uint32_t *d_mismatch,
+                            uint32_t *d_mismatch_count, uint32_t max_mismatch, size_t n, void *stream) {
+    if (!d_mismatch_count || !d_expected || (max_mismatch && !d_mismatch))
+        return ZDB_CRC32_EINVAL;
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    {
+        std::lock_guard<std::mutex> g(g_mu);
+        DeviceCtx *c;
+        int dev;
+        int rc = ensure_device(&c, &dev);
+        if (rc)
+            return rc;
+        if (hipMemsetAsync(d_mismatch_count, 0, sizeof(uint32_t), st) != hipSuccess)
+            return ZDB_CRC32_ELAUNCH;
+        if (n == 0)
+            return ZDB_CRC32_OK;
+        if (!d_arena || !d_offsets || !d_lengths || !d_out)
+            return ZDB_CRC32_EINVAL;
+        rc = enqueue_batch(*c, d_arena, d_offsets, d_lengths, d_out, n, st);
+        if (rc)
+            return rc;
+    }
+    const uint32_t blocks = (uint32_t)((n + 255) / 256);
+    hipLaunchKernelGGL(verify_kernel, dim3(blocks), dim3(256), 0, st, d_out, d_expected, (uint64_t)n,
+                       d_mismatch, d_mismatch_count, max_mismatch);
+    return hipGetLastError() == hipSuccess ? ZDB_CRC32_OK : ZDB_CRC32_ELAUNCH;
+}
+
+int zdb_crc32_batch(const uint8_t *arena, size_t arena_len, const uint64_t *offsets, const uint32_t *lengths,
+                    uint32_t *out, size_t n) {
+    if (n == 0)
+        return ZDB_CRC32_OK;
+    if (!arena || !offsets || !lengths || !out)
+        return ZDB_CRC32_EINVAL;
+    for (size_t r = 0; r < n; r++)
+        if (offsets[r] + lengths[r] > arena_len)
+            return ZDB_CRC32_EINVAL;
+    std::lock_guard<std::mutex> g(g_mu);
+    DeviceCtx *c;
+    int dev;
+    int rc = ensure_device(&c, &dev);
+    if (rc)
+        return rc;
+    HostStaging &h = g_host_staging[dev];
+    if (!h.st && hipStreamCreateWithFlags(&h.st, hipStreamNonBlocking) != hipSuccess)
+        return ZDB_CRC32_ELAUNCH;
+    const size_t abytes = arena_len + 16;
+    if (h.arena_bytes < abytes) {
+        if (h.arena)
+            hipFree(h.arena);
+        h.arena = nullptr;
+        if (hipMalloc(&h.arena, abytes) != hipSuccess) {
+            h.arena_bytes = 0;
+            return ZDB_CRC32_ENOMEM;
+        }
+        h.arena_bytes = abytes;
+    }
+    if (h.n_cap < n) {
+        hipFree(h.off);
+        hipFree(h.len);
+        hipFree(h.out);
+        h.off = nullptr;
+        h.len = nullptr;
+        h.out = nullptr;
+        if (hipMalloc(&h.off, n * 8) != hipSuccess || hipMalloc(&h.len, n * 4) != hipSuccess ||
+            hipMalloc(&h.out, n * 4) != hipSuccess) {
+            h.n_cap = 0;
+            return ZDB_CRC32_ENOMEM;
+        }
+        h.n_cap = n;
+    }
+    if (hipMemcpyAsync(h.arena, arena, arena_len, hipMemcpyHostToDevice, h.st) != hipSuccess ||
+        hipMemcpyAsync(h.off, offsets, n * 8, hipMemcpyHostToDevice, h.st) != hipSuccess ||
+        hipMemcpyAsync(h.len, lengths, n * 4, hipMemcpyHostToDevice, h.st) != hipSuccess)
+        return ZDB_CRC32_ELAUNCH;
+    rc = enqueue_batch(*c, h.arena, h.off, h.len, h.out, n, h.st);
+    if (rc)
+        return rc;
+    if (hipMemcpyAsync(out, h.out, n * 4, hipMemcpyDeviceToHost, h.st) != hipSuccess)
+        return ZDB_CRC32_ELAUNCH;
+    return hipStreamSynchronize(h.st) == hipSuccess ? ZDB_CRC32_OK : ZDB_CRC32_ELAUNCH;
+}
+
+void *zdb_crc32_host_alloc(size_t bytes) {
+    g_hip_touched = true;
+    void *p = nullptr;
+    if (hipHostMalloc(&p, bytes, hipHostMallocDefault) != hipSuccess)
+        return nullptr;
+    return p;
+}
+
+void zdb_crc32_host_free(void *p) {
+    if (p)
+        hipHostFree(p);
+}
+
+void zdb_crc32_set_timing(int enable) {
+    std::lock_guard<std::mutex> g(g_mu);
+    g_timing = enable != 0;
+}
+
+int zdb_crc32_kernel_stats(double *total_ms, uint64_t *launches) {
+    std::lock_guard<std::mutex> g(g_mu);
+    for (auto &p : g_pending) {
+        if (hipEventSynchronize(p.second) != hipSuccess)
+            return ZDB_CRC32_ELAUNCH;
+        float ms = 0;
+        hipEventElapsedTime(&ms, p.first, p.second);
+        g_time_ms += ms;
+        g_launches += 1;
+        g_event_pool.push_back(p.first);
+        g_event_pool.push_back(p.second);
+    }
+    g_pending.clear();
+    if (total_ms)
+        *total_ms = g_time_ms;
+    if (launches)
+        *launches = g_launches;
+    g_time_ms = 0;
+    g_launches = 0;
+    return ZDB_CRC32_OK;
+}
+
+int zdb_synth_fill_device(uint8_t *d_buf, size_t len, uint64_t seed, void *stream) {
+    if (!len)
+        return ZDB_CRC32_OK;
+    if (!d_buf || (reinterpret_cast<uintptr_t>(d_buf) & 7))
+        return ZDB_CRC32_EINVAL;
+    g_hip_touched = true;
+    hipLaunchKernelGGL(synth_kernel, dim3(8192), dim3(256), 0, static_cast<hipStream_t>(stream), d_buf,
+                       (uint64_t)len, seed);
+    return hipGetLastError() == hipSuccess ? ZDB_CRC32_OK : ZDB_CRC32_ELAUNCH;
+}
+
+} // extern "C"

@@ -1,0 +1,136 @@
+/*
+ * GF(2) toolkit and kernel table image -- see crc32c_gf2.h.
+ *
+ * Register convention is the reference's reflected one (crc32.c:16-91): bit 31
+ * of the register is the coefficient of x^0, and one zero-bit step is
+ * r = (r >> 1) ^ (r & 1 ? POLY : 0), i.e. a multiplication by x mod P.
+ */
+#include "crc32c_gf2.h"
+
+#include <pthread.h>
+#include <string.h>
+
+static uint32_t byte_table[256];
+static uint32_t xpow2[64];    /* x^(2^k) mod P             */
+static uint32_t xinvpow2[64]; /* x^(-(2^k)) mod P          */
+static pthread_once_t gf2_once = PTHREAD_ONCE_INIT;
+
+/* a * b mod P, both reflected (bit 31 = x^0) */
+static uint32_t multmodp(uint32_t a, uint32_t b) {
+    uint32_t m = 1u << 31, p = 0;
+    if (a == 0)
+        return 0;
+    for (;;) {
+        if (a & m) {
+            p ^= b;
+            if ((a & (m - 1)) == 0)
+                break;
+        }
+        m >>= 1;
+        b = (b & 1) ? (b >> 1) ^ ZDBCRC_POLY : (b >> 1);
+    }
+    return p;
+}
+
+/* inverse of the one-bit step: recovers r from (r >> 1) ^ (r & 1 ? P : 0).
+ * P has bit 31 set and (r >> 1) never does, so bit 31 tells the low bit. */
+static uint32_t unstep(uint32_t r) {
+    uint32_t lsb = r >> 31;
+    return ((r ^ (lsb ? ZDBCRC_POLY : 0)) << 1) | lsb;
+}
+
+static void gf2_init(void) {
+    for (uint32_t i = 0; i < 256; i++) {
+        uint32_t c = i;
+        for (int k = 0; k < 8; k++)
+            c = (c & 1) ? (c >> 1) ^ ZDBCRC_POLY : (c >> 1);
+        byte_table[i] = c;
+    }
+    xpow2[0] = 1u << 30;             /* x^1  */
+    xinvpow2[0] = unstep(1u << 31);  /* x^-1 */
+    for (int k = 1; k < 64; k++) {
+        xpow2[k] = multmodp(xpow2[k - 1], xpow2[k - 1]);
+        xinvpow2[k] = multmodp(xinvpow2[k - 1], xinvpow2[k - 1]);
+    }
+}
+
+static void gf2_ready(void) { pthread_once(&gf2_once, gf2_init); }
+
+/* x^e mod P (inverse powers when inv) */
+static uint32_t xpow(uint64_t e, int inv) {
+    const uint32_t *tab = inv ? xinvpow2 : xpow2;
+    uint32_t p = 1u << 31; /* x^0 */
+    for (int k = 0; e; k++, e >>= 1)
+        if (e & 1)
+            p = multmodp(tab[k], p);
+    return p;
+}
+
+uint32_t zdbcrc_shift(uint32_t crc, int64_t nbytes) {
+    gf2_ready();
+    if (nbytes == 0 || crc == 0)
+        return crc;
+    if (nbytes > 0)
+        return multmodp(xpow((uint64_t)nbytes * 8u, 0), crc);
+    return multmodp(xpow((uint64_t)(-nbytes) * 8u, 1), crc);
+}
+
+uint32_t zdbcrc_combine(uint32_t crc_a, uint32_t crc_b, uint64_t len_b) {
+    return zdbcrc_shift(crc_a, (int64_t)len_b) ^ crc_b;
+}
+
+uint32_t zdbcrc_update_bytes(uint32_t crc, const uint8_t *p, size_t n) {
+    gf2_ready();
+    for (size_t i = 0; i < n; i++)
+        crc = byte_table[(crc ^ p[i]) & 0xFF] ^ (crc >> 8);
+    return crc;
+}
+
+/* crc (from 0) of a 16-byte piece whose only set bits are (v << bit) */
+static uint32_t piece_slice_crc(uint32_t v, int bit) {
+    uint8_t piece[16];
+    memset(piece, 0, sizeof(piece));
+    for (int k = 0; k < 5; k++) {
+        int b = bit + k;
+        if (((v >> k) & 1) && b < 128)
+            piece[b >> 3] |= (uint8_t)(1u << (b & 7));
+    }
+    return zdbcrc_update_bytes(0, piece, 16);
+}
+
+/* register slice v at bit 5c, as a 32-bit value (bits past 31 dropped) */
+static uint32_t reg_slice(uint32_t v, int c) {
+    return (uint32_t)(((uint64_t)v << (5 * c)) & 0xFFFFFFFFu);
+}
+
+void zdbcrc_build_tables(uint32_t *img) {
+    gf2_ready();
+    memset(img, 0, sizeof(uint32_t) * ZDBCRC_TABLE_DW);
+
+    for (int i = 0; i < ZDBCRC_K; i++)
+        for (int c = 0; c < ZDBCRC_PCH; c++)
+            for (uint32_t v = 0; v < 32; v++)
+                img[ZDBCRC_OFF_T + (i * ZDBCRC_PCH + c) * 32 + v] =
+                    zdbcrc_shift(piece_slice_crc(v, 5 * c), 1024 * (int64_t)(ZDBCRC_K - 1 - i));
+
+    for (int c = 0; c < ZDBCRC_SCH; c++)
+        for (uint32_t v = 0; v < 32; v++)
+            img[ZDBCRC_OFF_W + c * 32 + v] = zdbcrc_shift(reg_slice(v, c), 1024 * ZDBCRC_K);
+
+    for (int c = 0; c < ZDBCRC_SCH; c++)
+        for (uint32_t v = 0; v < 32; v++)
+            for (int l = 0; l < ZDBCRC_WAVE; l++)
+                img[ZDBCRC_OFF_L + (c * 32 + v) * ZDBCRC_WAVE + l] =
+                    zdbcrc_shift(reg_slice(v, c), 16 * (int64_t)(ZDBCRC_WAVE - 1 - l));
+
+    for (int z = 0; z < 16; z++)
+        for (int c = 0; c < ZDBCRC_SCH; c++)
+            for (uint32_t v = 0; v < 32; v++)
+                img[ZDBCRC_OFF_Z + (z * ZDBCRC_SCH + c) * 32 + v] = zdbcrc_shift(reg_slice(v, c), -z);
+
+    for (int g = 0; g < ZDBCRC_GBITS; g++)
+        for (int c = 0; c < ZDBCRC_SCH; c++)
+            for (uint32_t v = 0; v < 32; v++)
+                img[ZDBCRC_OFF_G + (g * ZDBCRC_SCH + c) * 32 + v] =
+                    zdbcrc_shift(reg_slice(v, c), (int64_t)16 << g);
+}

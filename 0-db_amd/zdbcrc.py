@@ -1,0 +1,289 @@
+"""ctypes binding of libzdbcrc.so (the C ABI in include/zdb_crc32.h and
+include/zdb_datafile.h) for the Python test-suite, bench.py and
+__graft_entry__.py.
+
+The product is the C library; this module only marshals pointers.  It never
+computes a checksum itself and never falls back to anything: if the shared
+library is missing it raises at import, and every batched call raises
+``ZdbCrcError`` on a non-zero status.
+
+Device buffers are passed as torch tensors (torch is plumbing here: device
+memory, streams, torch.distributed); the library sees raw pointers and the
+raw hipStream_t of torch's current stream.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from pathlib import Path
+
+import numpy as np
+
+HERE = Path(__file__).resolve().parent
+LIB_PATH = Path(os.environ.get("ZDBCRC_LIB", HERE / "lib" / "libzdbcrc.so"))
+
+if not LIB_PATH.exists():
+    raise ImportError(
+        f"libzdbcrc.so not found at {LIB_PATH}: build it with `make -C 0-db_amd` "
+        "(or __graft_entry__.build()); there is no fallback implementation")
+
+_lib = C.CDLL(str(LIB_PATH))
+
+u8p = C.POINTER(C.c_uint8)
+vp = C.c_void_p
+
+
+def _fn(name, restype, *argtypes):
+    f = getattr(_lib, name)
+    f.restype = restype
+    f.argtypes = list(argtypes)
+    return f
+
+
+# scalar drop-ins (crc32.h:5,8; api.h:72)
+_engine_value = _fn("zdb_crc32_engine_value", C.c_char_p)
+_crc32 = _fn("zdb_crc32", C.c_uint32, vp, C.c_ssize_t)
+_checksum = _fn("zdb_checksum_crc32", C.c_uint32, vp, C.c_ssize_t)
+_shift = _fn("zdb_crc32_shift", C.c_uint32, C.c_uint32, C.c_int64)
+_combine = _fn("zdb_crc32_combine", C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint64)
+_table_image = _fn("zdb_crc32_table_image", C.c_size_t, vp, C.c_size_t)
+
+# batched GPU entries
+_strerror = _fn("zdb_crc32_strerror", C.c_char_p, C.c_int)
+_batch_engine = _fn("zdb_crc32_batch_engine", C.c_char_p)
+_gpu_initialized = _fn("zdb_crc32_gpu_initialized", C.c_int)
+_batch_device = _fn("zdb_crc32_batch_device", C.c_int, vp, vp, vp, vp, C.c_size_t, vp)
+_verify_device = _fn("zdb_crc32_verify_device", C.c_int, vp, vp, vp, vp, vp, vp, vp, C.c_uint32,
+                     C.c_size_t, vp)
+_batch_host = _fn("zdb_crc32_batch", C.c_int, vp, C.c_size_t, vp, vp, vp, C.c_size_t)
+_host_alloc = _fn("zdb_crc32_host_alloc", vp, C.c_size_t)
+_host_free = _fn("zdb_crc32_host_free", None, vp)
+_set_timing = _fn("zdb_crc32_set_timing", None, C.c_int)
+_kernel_stats = _fn("zdb_crc32_kernel_stats", C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_uint64))
+
+# synthetic inputs
+_synth_fill = _fn("zdb_synth_fill", None, vp, C.c_size_t, C.c_uint64)
+_synth_fill_device = _fn("zdb_synth_fill_device", C.c_int, vp, C.c_size_t, C.c_uint64, vp)
+_zipf = _fn("zdb_synth_zipf_lengths", C.c_size_t, vp, C.c_size_t, C.c_uint64, C.c_uint64)
+
+# datafile framing
+_walk = _fn("zdb_datafile_walk", C.c_long, vp, C.c_size_t, vp, C.c_long, C.POINTER(C.c_int))
+_encode_entry = _fn("zdb_datafile_encode_entry", C.c_size_t, vp, vp, C.c_uint8, C.c_uint32, C.c_uint32,
+                    C.c_uint32, C.c_uint8, C.c_uint32)
+_encode_header = _fn("zdb_datafile_encode_header", C.c_size_t, vp, C.c_uint32)
+
+#: every symbol include/*.h declares (checked by tests/test_abi.py)
+EXPORTED = [
+    "zdb_crc32_engine_value", "zdb_crc32", "zdb_checksum_crc32", "zdb_crc32_shift",
+    "zdb_crc32_combine", "zdb_crc32_table_image", "zdb_crc32_strerror", "zdb_crc32_batch_engine",
+    "zdb_crc32_gpu_initialized", "zdb_crc32_batch_device", "zdb_crc32_verify_device",
+    "zdb_crc32_batch", "zdb_crc32_host_alloc", "zdb_crc32_host_free", "zdb_crc32_set_timing",
+    "zdb_crc32_kernel_stats", "zdb_synth_fill", "zdb_synth_fill_device", "zdb_synth_zipf_lengths",
+    "zdb_datafile_walk", "zdb_datafile_encode_entry", "zdb_datafile_encode_header",
+    "zdb_datafile_payloads",
+]
+
+RECORD_DTYPE = np.dtype([
+    ("header_offset", "<u8"), ("payload_offset", "<u8"), ("datalength", "<u4"),
+    ("integrity", "<u4"), ("previous", "<u4"), ("timestamp", "<u4"), ("idlength", "u1"),
+    ("flags", "u1"), ("pad", "u1", (6,)),
+])
+assert RECORD_DTYPE.itemsize == 40
+
+WALK_OK, WALK_SHORT_HEADER, WALK_SHORT_PAYLOAD, WALK_BAD_DESCRIPTOR = 0, 1, 2, 3
+
+
+class ZdbCrcError(RuntimeError):
+    pass
+
+
+def _check(rc: int, what: str):
+    if rc != 0:
+        raise ZdbCrcError(f"{what}: {_strerror(rc).decode()} ({rc})")
+
+
+def _ptr(buf) -> int:
+    if isinstance(buf, np.ndarray):
+        if not buf.flags["C_CONTIGUOUS"]:
+            raise ValueError("array must be C-contiguous")
+        return buf.ctypes.data
+    if isinstance(buf, (bytes, bytearray, memoryview)):
+        arr = np.frombuffer(buf, dtype=np.uint8)
+        return arr.ctypes.data
+    raise TypeError(type(buf))
+
+
+# ---------------------------------------------------------------- scalar --
+
+def engine_value() -> str:
+    return _engine_value().decode()
+
+
+def crc32(data) -> int:
+    arr = np.frombuffer(bytes(data), dtype=np.uint8) if not isinstance(data, np.ndarray) else data
+    return int(_crc32(arr.ctypes.data if arr.size else None, arr.size))
+
+
+def checksum_crc32(data) -> int:
+    arr = np.frombuffer(bytes(data), dtype=np.uint8) if not isinstance(data, np.ndarray) else data
+    return int(_checksum(arr.ctypes.data if arr.size else None, arr.size))
+
+
+def shift(crc: int, nbytes: int) -> int:
+    return int(_shift(crc, nbytes))
+
+
+def combine(crc_a: int, crc_b: int, len_b: int) -> int:
+    return int(_combine(crc_a, crc_b, len_b))
+
+
+def table_image() -> np.ndarray:
+    n = _table_image(None, 0)
+    img = np.zeros(n, dtype=np.uint32)
+    _table_image(img.ctypes.data, n)
+    return img
+
+
+# ----------------------------------------------------------------- batch --
+
+def batch_engine() -> str:
+    return _batch_engine().decode()
+
+
+def gpu_initialized() -> bool:
+    return bool(_gpu_initialized())
+
+
+def _stream_handle(stream) -> int | None:
+    import torch
+    if stream is None:
+        stream = torch.cuda.current_stream()
+    return stream.cuda_stream
+
+
+def _dev_check(t, dtype, name):
+    import torch
+    if not t.is_cuda:
+        raise ValueError(f"{name} must be a device tensor")
+    if t.dtype != dtype:
+        raise ValueError(f"{name} must be {dtype}, got {t.dtype}")
+    if not t.is_contiguous():
+        raise ValueError(f"{name} must be contiguous")
+    return t
+
+
+def batch_device(arena, offsets, lengths, out, stream=None):
+    """out[r] = zdb_crc32(arena[offsets[r]:][:lengths[r]]) on the GPU (async)."""
+    import torch
+    _dev_check(arena, torch.uint8, "arena")
+    _dev_check(offsets, torch.int64, "offsets")
+    _dev_check(lengths, torch.int32, "lengths")
+    _dev_check(out, torch.int32, "out")
+    n = offsets.numel()
+    if lengths.numel() != n or out.numel() < n:
+        raise ValueError("descriptor sizes differ")
+    _check(_batch_device(arena.data_ptr(), offsets.data_ptr(), lengths.data_ptr(), out.data_ptr(), n,
+                         _stream_handle(stream)), "zdb_crc32_batch_device")
+    return out
+
+
+def verify_device(arena, offsets, lengths, expected, out, mismatch, count, stream=None):
+    import torch
+    for t, d, nm in ((arena, torch.uint8, "arena"), (offsets, torch.int64, "offsets"),
+                     (lengths, torch.int32, "lengths"), (expected, torch.int32, "expected"),
+                     (out, torch.int32, "out"), (mismatch, torch.int32, "mismatch"),
+                     (count, torch.int32, "count")):
+        _dev_check(t, d, nm)
+    n = offsets.numel()
+    _check(_verify_device(arena.data_ptr(), offsets.data_ptr(), lengths.data_ptr(), expected.data_ptr(),
+                          out.data_ptr(), mismatch.data_ptr(), count.data_ptr(), mismatch.numel(), n,
+                          _stream_handle(stream)), "zdb_crc32_verify_device")
+
+
+def batch_host(arena: np.ndarray, offsets: np.ndarray, lengths: np.ndarray) -> np.ndarray:
+    """Host buffers in, host crcs out (H2D + kernel + D2H, synchronous)."""
+    arena = np.ascontiguousarray(arena, dtype=np.uint8)
+    offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+    lengths = np.ascontiguousarray(lengths, dtype=np.uint32)
+    out = np.zeros(len(offsets), dtype=np.uint32)
+    _check(_batch_host(arena.ctypes.data, arena.size, offsets.ctypes.data, lengths.ctypes.data,
+                       out.ctypes.data, len(offsets)), "zdb_crc32_batch")
+    return out
+
+
+class PinnedBuffer:
+    """Pinned host staging (zdb_crc32_host_alloc) exposed as a numpy array."""
+
+    def __init__(self, nbytes: int):
+        self.nbytes = nbytes
+        self.ptr = _host_alloc(nbytes)
+        if not self.ptr:
+            raise ZdbCrcError("zdb_crc32_host_alloc failed")
+        self.array = np.ctypeslib.as_array((C.c_uint8 * nbytes).from_address(self.ptr))
+
+    def free(self):
+        if self.ptr:
+            _host_free(self.ptr)
+            self.ptr = None
+
+
+def set_timing(enable: bool):
+    _set_timing(1 if enable else 0)
+
+
+def kernel_stats():
+    ms = C.c_double(0)
+    n = C.c_uint64(0)
+    _check(_kernel_stats(C.byref(ms), C.byref(n)), "zdb_crc32_kernel_stats")
+    return ms.value, n.value
+
+
+# ------------------------------------------------------------- synthetic --
+
+def synth_fill(nbytes: int, seed: int) -> np.ndarray:
+    buf = np.empty(nbytes, dtype=np.uint8)
+    if nbytes:
+        _synth_fill(buf.ctypes.data, nbytes, seed)
+    return buf
+
+
+def synth_fill_device(t, seed: int, stream=None):
+    import torch
+    _dev_check(t, torch.uint8, "buffer")
+    _check(_synth_fill_device(t.data_ptr(), t.numel(), seed, _stream_handle(stream)),
+           "zdb_synth_fill_device")
+
+
+def zipf_lengths(target_bytes: int, seed: int, max_n: int | None = None) -> np.ndarray:
+    if max_n is None:
+        max_n = max(16, target_bytes // 64 + 16)
+    out = np.empty(max_n, dtype=np.uint32)
+    n = _zipf(out.ctypes.data, max_n, target_bytes, seed)
+    return out[:n].copy()
+
+
+# -------------------------------------------------------------- datafile --
+
+def datafile_walk(image) -> tuple[np.ndarray, int]:
+    img = np.frombuffer(image, dtype=np.uint8) if not isinstance(image, np.ndarray) else image
+    st = C.c_int(0)
+    n = _walk(img.ctypes.data, img.size, None, 0, C.byref(st))
+    recs = np.zeros(max(n, 1), dtype=RECORD_DTYPE)
+    n2 = _walk(img.ctypes.data, img.size, recs.ctypes.data, n, C.byref(st))
+    assert n2 == n
+    return recs[:n], st.value
+
+
+def encode_header(fileid: int = 0) -> bytes:
+    buf = np.zeros(28, dtype=np.uint8)
+    _encode_header(buf.ctypes.data, fileid)
+    return buf.tobytes()
+
+
+def encode_entry(key: bytes, datalength: int, previous: int, integrity: int, flags: int = 0,
+                 timestamp: int = 0) -> bytes:
+    buf = np.zeros(18 + len(key), dtype=np.uint8)
+    k = np.frombuffer(key, dtype=np.uint8) if key else None
+    n = _encode_entry(buf.ctypes.data, k.ctypes.data if k is not None else None, len(key), datalength,
+                      previous, integrity, flags, timestamp)
+    return buf[:n].tobytes()

@@ -1,0 +1,128 @@
+/*
+ * zdb_crc32.h -- C ABI of the MI355X-native batched record checksum for 0-db.
+ *
+ * Library: 0-db_amd/lib/libzdbcrc.so (build: make -C 0-db_amd).
+ * No torch types, no HIP types: plain pointers, sizes and an opaque stream.
+ *
+ * Checksum function everywhere: 0-db's "crc32" = CRC-32C (reflected poly
+ * 0x82F63B78) with initial register 0 and NO final XOR (libzdb/crc32.c:84-110).
+ * It is not the standard CRC-32C ("123456789" -> 0x58e3fa20, not 0xe3069283).
+ */
+#ifndef ZDB_CRC32_AMD_H
+#define ZDB_CRC32_AMD_H
+
+#include <stdint.h>
+#include <stddef.h>
+#include <sys/types.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ------------------------------------------------------------------------
+ * 1. Drop-in scalar entry points (CPU only, never initialise the GPU).
+ *    Bit-exact replacements for the reference symbols; link this library (or
+ *    its crc32_cpu.o) in place of libzdb/crc32.o.
+ * ------------------------------------------------------------------------ */
+
+/* replaces crc32.h:5 / crc32.c:133-143 -- "sse42" or "software" */
+char *zdb_crc32_engine_value();
+
+/* replaces crc32.h:8 / crc32.c:145-155; length <= 0 returns 0 */
+uint32_t zdb_crc32(const uint8_t *bytes, ssize_t length);
+
+/* replaces api.h:72 / api.c:470-472 (the tools' entry point) */
+uint32_t zdb_checksum_crc32(const uint8_t *bytes, ssize_t length);
+
+/* GF(2) helpers (new): register advanced over nbytes zero bytes (nbytes < 0
+ * applies the inverse), and crc(A||B) from crc(A), crc(B), |B|. */
+uint32_t zdb_crc32_shift(uint32_t crc, int64_t nbytes);
+uint32_t zdb_crc32_combine(uint32_t crc_a, uint32_t crc_b, uint64_t len_b);
+
+/* Introspection: writes the host-built table image that the kernel stages
+ * (layout: 0-db_amd/csrc/crc32c_gf2.h) when dwords is large enough; returns
+ * the image size in dwords.  Used by the CPU model of the kernel in tests. */
+size_t zdb_crc32_table_image(uint32_t *dst, size_t dwords);
+
+/* ------------------------------------------------------------------------
+ * 2. Batched GPU entry points (new, additive).
+ *    One call checksums n independent records of an arena:
+ *        out[r] = zdb_crc32(arena + offsets[r], lengths[r])
+ *    This is the batched form of every payload caller: SET
+ *    (commands_set.c:106, :216; api.c:124, :204), CHECK (data.c:564) and the
+ *    integrity scan (integrity-check.c:90).
+ *    HIP is initialised lazily on the first batched call (after any fork).
+ *    Errors are returned, never hidden: there is no CPU fallback inside.
+ * ------------------------------------------------------------------------ */
+
+#define ZDB_CRC32_OK            0
+#define ZDB_CRC32_ENODEV       -1  /* no usable gfx950 device / HIP runtime */
+#define ZDB_CRC32_EINVAL       -2  /* bad argument                          */
+#define ZDB_CRC32_ENOMEM       -3  /* device allocation failed              */
+#define ZDB_CRC32_ELAUNCH      -4  /* kernel launch / runtime error         */
+
+const char *zdb_crc32_strerror(int code);
+
+/* "hip-gfx950" once a device is bound, "uninitialized" before */
+const char *zdb_crc32_batch_engine(void);
+
+/* 1 when this process has initialised HIP through this library */
+int zdb_crc32_gpu_initialized(void);
+
+/* Device-resident batch.  All pointers are device pointers on the calling
+ * thread's current HIP device; `stream` is a hipStream_t (NULL = default
+ * stream).  Asynchronous: results are valid once the stream has reached the
+ * point of the call.  Records may start and end at any byte alignment and may
+ * overlap; lengths may be 0 (crc 0).  The arena must stay readable up to the
+ * 16-byte boundary that follows each record's last byte (true for any
+ * allocation from hipMalloc). */
+int zdb_crc32_batch_device(const uint8_t *d_arena, const uint64_t *d_offsets,
+                           const uint32_t *d_lengths, uint32_t *d_out,
+                           size_t n, void *stream);
+
+/* Device-resident verify: as zdb_crc32_batch_device, then compares with
+ * d_expected[r] (the stored `integrity` field, data.h:60).  Mismatching record
+ * indices are appended (unordered) to d_mismatch[0..max_mismatch) and
+ * counted in *d_mismatch_count (device u32, zeroed by this call). */
+int zdb_crc32_verify_device(const uint8_t *d_arena, const uint64_t *d_offsets,
+                            const uint32_t *d_lengths, const uint32_t *d_expected,
+                            uint32_t *d_out, uint32_t *d_mismatch,
+                            uint32_t *d_mismatch_count, uint32_t max_mismatch,
+                            size_t n, void *stream);
+
+/* Host-buffer batch: copies arena[0..arena_len) and the descriptors to the
+ * device, runs, copies out[] back, and synchronises.  Pinned host memory
+ * (zdb_crc32_host_alloc) gives full PCIe rate. */
+int zdb_crc32_batch(const uint8_t *arena, size_t arena_len, const uint64_t *offsets,
+                    const uint32_t *lengths, uint32_t *out, size_t n);
+
+/* pinned host staging for the host-buffer path */
+void *zdb_crc32_host_alloc(size_t bytes);
+void zdb_crc32_host_free(void *p);
+
+/* Instrumentation: when enabled, the main kernel of every batched call is
+ * bracketed by HIP events on the caller's stream; the accumulated time of
+ * completed launches is returned by zdb_crc32_kernel_stats (synchronises on
+ * the recorded events). */
+void zdb_crc32_set_timing(int enable);
+int zdb_crc32_kernel_stats(double *total_ms, uint64_t *launches);
+
+/* ------------------------------------------------------------------------
+ * 3. Deterministic synthetic inputs (bench / tests on both hosts).
+ *    Byte i of a filled buffer is byte (i mod 8) of the little-endian word
+ *    splitmix64_mix(seed + (i/8 + 1) * 0x9E3779B97F4A7C15).
+ * ------------------------------------------------------------------------ */
+void zdb_synth_fill(uint8_t *buf, size_t len, uint64_t seed);
+int zdb_synth_fill_device(uint8_t *d_buf, size_t len, uint64_t seed, void *stream);
+
+/* SURVEY §8(d) C3 recipe: bucket k in 0..14 with P(k) ~ (k+1)^-1.1, size
+ * uniform in [64*2^k, 64*2^(k+1)), capped at 1 MiB, drawn until the running
+ * total reaches target_bytes (or max_n records).  Returns the count. */
+size_t zdb_synth_zipf_lengths(uint32_t *lengths, size_t max_n,
+                              uint64_t target_bytes, uint64_t seed);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif

@@ -1,0 +1,75 @@
+/*
+ * zdb_datafile.h -- 0-db datafile framing and the host-side record walk that
+ * feeds the batched GPU checksum (library: 0-db_amd/lib/libzdbcrc.so).
+ *
+ * On-disk format, datafile version 3 (libzdb/libzdb.h:29), little endian,
+ * packed:
+ *   data_header_t       (libzdb/data.h:38-45) 28 bytes: "DAT0", u32 version,
+ *                        u64 created, u64 opened, u32 fileid
+ *   data_entry_header_t (libzdb/data.h:56-65) 18 bytes: u8 idlength,
+ *                        u32 datalength, u32 previous, u32 integrity,
+ *                        u8 flags, u32 timestamp; then id[idlength], then
+ *                        datalength payload bytes.
+ * `integrity` (byte 9 of the entry header) is zdb_crc32(payload).
+ */
+#ifndef ZDB_DATAFILE_AMD_H
+#define ZDB_DATAFILE_AMD_H
+
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ZDB_DATAFILE_VERSION   3
+#define ZDB_DATA_HEADER_SIZE  28
+#define ZDB_ENTRY_HEADER_SIZE 18
+#define ZDB_ENTRY_DELETED      1  /* data.h:48 */
+#define ZDB_ENTRY_TRUNCATED    2  /* data.h:49 */
+
+typedef struct zdb_record_t {
+    uint64_t header_offset;   /* offset of the entry header in the file   */
+    uint64_t payload_offset;  /* offset of the payload                    */
+    uint32_t datalength;      /* payload bytes                            */
+    uint32_t integrity;       /* stored crc                               */
+    uint32_t previous;        /* previous entry offset                    */
+    uint32_t timestamp;
+    uint8_t idlength;
+    uint8_t flags;
+    uint8_t pad[6];
+} zdb_record_t;
+
+/* walk status, mirroring how tools/integrity-check stops */
+#define ZDB_WALK_OK             0  /* clean end of file (integrity-check.c:59)        */
+#define ZDB_WALK_SHORT_HEADER   1  /* "data header read failed" (:68-69)              */
+#define ZDB_WALK_SHORT_PAYLOAD  2  /* "payload entry read failed" (:87-88)            */
+#define ZDB_WALK_BAD_DESCRIPTOR 3  /* short file header, magic or version (data.c:197-206) */
+
+/* Walk the entry headers of an in-memory datafile image (the serial chain of
+ * integrity-check.c:59-69 / data.c:306-311).  Fills up to max_records
+ * descriptors in file order and returns the number of records walked
+ * (including the one that stopped a SHORT_PAYLOAD walk); pass recs = NULL to
+ * count only. */
+long zdb_datafile_walk(const uint8_t *image, size_t len, zdb_record_t *recs, long max_records,
+                       int *status);
+
+/* Encode one entry header + key at dst (data_insert, data.c:594-633; the
+ * caller passes the payload crc, as data.c:606 takes source->crc).  Returns
+ * bytes written (18 + idlength). */
+size_t zdb_datafile_encode_entry(uint8_t *dst, const uint8_t *id, uint8_t idlength, uint32_t datalength,
+                                 uint32_t previous, uint32_t integrity, uint8_t flags, uint32_t timestamp);
+
+/* Encode the 28-byte file header (data_initialize, data.c: created/opened 0). */
+size_t zdb_datafile_encode_header(uint8_t *dst, uint32_t fileid);
+
+/* Gather descriptors for the batched checksum: records with datalength > 0
+ * (integrity-check.c:81-82 skips empty ones).  Returns the count written. */
+size_t zdb_datafile_payloads(const zdb_record_t *recs, size_t nrecs, uint64_t *offsets, uint32_t *lengths,
+                             uint32_t *expected, uint32_t *record_index);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif
