@@ -1,0 +1,148 @@
+"""CPU model of crc_batch_kernel (0-db_amd/csrc/crc32_hip.hip), in numpy.
+
+It replays the kernel's exact algorithm -- unit scan, per-wave unit slices,
+segment walk, end-aligned lane mapping, supersteps of K slots, 5-bit table
+lookups from the host-built table image, lane placement, trailing-pad removal
+and the generic piece shift -- so the math can be checked against the oracle
+on a machine without a GPU.  The GPU tests then check the HIP code itself.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+K, PCH, SCH, WAVE = 4, 26, 7, 64
+OFF_T = 0
+OFF_W = OFF_T + K * PCH * 32
+OFF_L = OFF_W + SCH * 32
+LDS_DW = OFF_L + SCH * 32 * WAVE
+OFF_Z = LDS_DW
+OFF_G = OFF_Z + 16 * SCH * 32
+GBITS = 32
+TABLE_DW = OFF_G + GBITS * SCH * 32
+UNIT_OVH = 16
+MIN_UNITS_PER_WAVE = 256
+
+LANES = np.arange(WAVE, dtype=np.int64)
+
+
+def _slices128(words: np.ndarray) -> np.ndarray:
+    """words: [64, 4] uint32 -> [64, 26] 5-bit slices of the 128-bit piece."""
+    w = words.astype(object)
+    big = w[:, 0] | (w[:, 1] << 32) | (w[:, 2] << 64) | (w[:, 3] << 96)
+    out = np.zeros((len(words), PCH), dtype=np.int64)
+    for c in range(PCH):
+        out[:, c] = [int((b >> (5 * c)) & 31) for b in big]
+    return out
+
+
+def _slices32(x: np.ndarray) -> np.ndarray:
+    x = x.astype(np.uint64)
+    return np.stack([((x >> np.uint64(5 * c)) & np.uint64(31)).astype(np.int64) for c in range(SCH)], 1)
+
+
+def _uniform_shift(x: int, tab: np.ndarray, base: int) -> int:
+    r = 0
+    for c in range(SCH):
+        r ^= int(tab[base + c * 32 + ((x >> (5 * c)) & 31)])
+    return r
+
+
+def _keep_mask(lo: int, hi: int, k: int) -> int:
+    a, b = lo - 4 * k, hi - 4 * k
+    mh = 0xFFFFFFFF if b >= 4 else 0 if b <= 0 else (1 << (8 * b)) - 1
+    ml = 0xFFFFFFFF if a <= 0 else 0 if a >= 4 else (0xFFFFFFFF << (8 * a)) & 0xFFFFFFFF
+    return mh & ml
+
+
+def segment_crc(mem: np.ndarray, base_addr: int, P0: int, pa: int, pb: int, np_: int, lo0: int,
+                hi_last: int, tab: np.ndarray) -> int:
+    nps = pb - pa
+    T = (nps + 63) // 64
+    S = (T + K - 1) // K
+    t0 = S * K - T
+    base_j = pb - 64 * S * K
+    acc = np.zeros(WAVE, dtype=np.uint32)
+    for ss in range(S):
+        if ss:
+            sl = _slices32(acc)
+            acc = np.bitwise_xor.reduce(tab[OFF_W + np.arange(SCH) * 32 + sl], axis=1).astype(np.uint32)
+        for i in range(K):
+            t = ss * K + i
+            if t < t0:
+                continue
+            jj = base_j + 64 * t + LANES
+            words = np.zeros((WAVE, 4), dtype=np.uint32)
+            for l in range(WAVE):
+                j = int(jj[l])
+                if j < pa:
+                    continue
+                addr = P0 + 16 * j - base_addr
+                wv = mem[addr:addr + 16].view("<u4").copy()
+                if j == 0 or j == np_ - 1:
+                    lo = lo0 if j == 0 else 0
+                    hi = hi_last if j == np_ - 1 else 16
+                    for k in range(4):
+                        wv[k] &= np.uint32(_keep_mask(lo, hi, k))
+                words[l] = wv
+            sl = _slices128(words)
+            idx = OFF_T + (i * PCH + np.arange(PCH)) * 32 + sl
+            acc ^= np.bitwise_xor.reduce(tab[idx], axis=1).astype(np.uint32)
+    sl = _slices32(acc)
+    idx = OFF_L + (np.arange(SCH)[None, :] * 32 + sl) * WAVE + LANES[:, None]
+    placed = np.bitwise_xor.reduce(tab[idx], axis=1)
+    return int(np.bitwise_xor.reduce(placed))
+
+
+def batch(arena: np.ndarray, offsets, lengths, tab: np.ndarray, max_waves: int = 4096,
+          min_units: int = MIN_UNITS_PER_WAVE, base_addr: int = 0) -> np.ndarray:
+    """out[r] as crc_batch_kernel computes it.  base_addr is the (virtual)
+    address of arena[0]; pieces are aligned on absolute addresses."""
+    offsets = np.asarray(offsets, dtype=np.int64)
+    lengths = np.asarray(lengths, dtype=np.int64)
+    n = len(offsets)
+    out = np.zeros(n, dtype=np.uint32)
+    if n == 0:
+        return out
+    # memory with slack so aligned reads never leave the buffer
+    pad_lo = (base_addr & 15) + 16
+    mem = np.zeros(pad_lo + len(arena) + 32, dtype=np.uint8)
+    mem[pad_lo:pad_lo + len(arena)] = arena
+    mem_base = base_addr - pad_lo  # absolute address of mem[0]
+
+    A = base_addr + offsets
+    units = np.where(lengths > 0, ((A + lengths - 1) >> 4) - (A >> 4) + 1, 0) + UNIT_OVH
+    unit_start = np.zeros(n + 1, dtype=np.int64)
+    unit_start[1:] = np.cumsum(units)
+    total = int(unit_start[n])
+    nwaves = min(max_waves, (total + min_units - 1) // min_units)
+    for gw in range(nwaves):
+        ub = total * gw // nwaves
+        ue = total * (gw + 1) // nwaves
+        if ub >= ue:
+            continue
+        r = int(np.searchsorted(unit_start, ub, side="right") - 1)
+        while True:
+            us = int(unit_start[r]) + UNIT_OVH
+            ur = int(unit_start[r + 1])
+            s_lo, s_hi = max(ub, us), min(ue, ur)
+            if s_hi > s_lo:
+                a = int(A[r])
+                aend = a + int(lengths[r])
+                P0 = a & ~15
+                np_ = ur - us
+                z = P0 + 16 * np_ - aend
+                pa, pb = s_lo - us, s_hi - us
+                x = segment_crc(mem, mem_base, P0, pa, pb, np_, a & 15, 16 - z, tab)
+                if z:
+                    x = _uniform_shift(x, tab, OFF_Z + z * SCH * 32)
+                q, g = np_ - pb, 0
+                while q:
+                    if q & 1:
+                        x = _uniform_shift(x, tab, OFF_G + g * SCH * 32)
+                    q >>= 1
+                    g += 1
+                out[r] ^= np.uint32(x)  # store for whole records == xor into 0
+            if ur >= ue or r + 1 >= n:
+                break
+            r += 1
+    return out

@@ -1,0 +1,235 @@
+"""GPU parity tests: the HIP path (through the C ABI) against the oracle and
+the reference-generated golden fixtures.  Bit-exact everywhere (integer
+work).  Run on an MI355X with `pytest -m gpu`."""
+from __future__ import annotations
+
+import os
+import shutil
+import subprocess
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+import oracle
+from conftest import GOLDEN, ROOT, kat_bytes
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+
+@pytest.fixture(scope="module")
+def dev():
+    if not torch.cuda.is_available():
+        pytest.fail("no GPU visible to torch (tests marked gpu must run on the MI355X box)")
+    import zdbcrc
+    return zdbcrc
+
+
+def gpu_batch(zdbcrc, arena: np.ndarray, offs, lens, pad: int = 64) -> np.ndarray:
+    a = torch.zeros(len(arena) + pad, dtype=torch.uint8, device="cuda")
+    if len(arena):
+        a[: len(arena)] = torch.from_numpy(np.ascontiguousarray(arena)).cuda()
+    o = torch.from_numpy(np.asarray(offs, dtype=np.int64)).cuda()
+    l = torch.from_numpy(np.asarray(lens, dtype=np.int64).astype(np.int32)).cuda()
+    out = torch.full((len(o),), -1, dtype=torch.int32, device="cuda")
+    zdbcrc.batch_device(a, o, l, out)
+    torch.cuda.synchronize()
+    return out.cpu().numpy().view(np.uint32)
+
+
+def test_engine_binds(dev):
+    gpu_batch(dev, np.zeros(16, np.uint8), [0], [16])
+    assert dev.batch_engine() == "hip-gfx950"
+    assert dev.gpu_initialized()
+
+
+def test_known_answers(dev, kats):
+    blobs = [kat_bytes(e) for e in kats]
+    offs, pos = [], 0
+    for b in blobs:
+        offs.append(pos)
+        pos += len(b) + 5  # odd gaps: every record at a different alignment
+    arena = np.zeros(pos, np.uint8)
+    for o, b in zip(offs, blobs):
+        arena[o:o + len(b)] = np.frombuffer(b, np.uint8)
+    got = gpu_batch(dev, arena, offs, [len(b) for b in blobs])
+    for e, g in zip(kats, got):
+        assert g == int(e["crc"], 16), e["name"]
+
+
+def test_vectors_every_alignment(dev, vectors):
+    """1546 reference vectors (0..4160 B and up to 1 MiB), each placed at all
+    16 start alignments in one batch."""
+    lens, seeds, crcs = vectors
+    offs, blobs, pos = [], [], 0
+    for n, s in zip(lens, seeds):
+        data = oracle.splitmix_bytes(int(n), int(s))
+        for mis in range(16):
+            pos = (pos + 15) // 16 * 16 + mis
+            offs.append(pos)
+            blobs.append(data)
+            pos += int(n)
+    arena = np.zeros(pos + 16, np.uint8)
+    for o, b in zip(offs, blobs):
+        arena[o:o + len(b)] = b
+    got = gpu_batch(dev, arena, offs, [len(b) for b in blobs])
+    np.testing.assert_array_equal(got, np.repeat(crcs, 16))
+
+
+@pytest.mark.parametrize("seed,nrec,maxlen", [(1, 3000, 200), (2, 2000, 5000), (3, 400, 70_000),
+                                              (4, 40, 3_000_000), (5, 1, 8 << 20)])
+def test_random_batches(dev, oracle_c, seed, nrec, maxlen):
+    rng = np.random.default_rng(seed)
+    lens = rng.integers(0, maxlen + 1, nrec)
+    span = int(lens.sum()) // 2 + maxlen + 1
+    arena = oracle.splitmix_bytes(span, seed)
+    offs = np.array([rng.integers(0, span - l + 1) for l in lens])  # overlapping records
+    np.testing.assert_array_equal(gpu_batch(dev, arena, offs, lens), oracle_c.batch(arena, offs, lens))
+
+
+def test_overlapping_and_empty(dev, oracle_c):
+    arena = oracle.splitmix_bytes(100_000, 77)
+    offs = [0, 0, 1, 0, 50_000, 99_999, 12_345, 12_345]
+    lens = [100_000, 0, 99_999, 1, 0, 1, 65_536, 65_537]
+    np.testing.assert_array_equal(gpu_batch(dev, arena, offs, lens), oracle_c.batch(arena, offs, lens))
+
+
+def test_split_heavy_geometry(dev, oracle_c):
+    """One huge record among thousands of tiny ones: forces slices of the unit
+    space to cut records (atomic XOR recombination) and tiny-record walks."""
+    rng = np.random.default_rng(9)
+    lens = np.concatenate([rng.integers(1, 64, 20_000), [7 << 20], rng.integers(1, 300, 5000)])
+    offs = np.zeros(len(lens), np.int64)
+    offs[1:] = np.cumsum(lens[:-1])
+    arena = oracle.splitmix_bytes(int(lens.sum()), 10)
+    np.testing.assert_array_equal(gpu_batch(dev, arena, offs, lens), oracle_c.batch(arena, offs, lens))
+
+
+def test_device_arena_unaligned_base(dev, oracle_c):
+    arena = oracle.splitmix_bytes(300_000, 12)
+    rng = np.random.default_rng(12)
+    lens = rng.integers(0, 20_000, 200)
+    offs = np.array([rng.integers(0, 300_000 - l - 8) for l in lens])
+    a = torch.zeros(300_064, dtype=torch.uint8, device="cuda")
+    a[3:300_003] = torch.from_numpy(arena).cuda()
+    view = a[3:]  # data_ptr() = base + 3
+    o = torch.from_numpy(offs.astype(np.int64)).cuda()
+    l = torch.from_numpy(lens.astype(np.int32)).cuda()
+    out = torch.zeros(len(offs), dtype=torch.int32, device="cuda")
+    dev.batch_device(view, o, l, out)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(out.cpu().numpy().view(np.uint32), oracle_c.batch(arena, offs, lens))
+
+
+def test_verify_reports_mismatches(dev, oracle_c):
+    arena = oracle.splitmix_bytes(200_000, 13)
+    rng = np.random.default_rng(13)
+    lens = rng.integers(1, 3000, 500)
+    offs = np.array([rng.integers(0, 200_000 - l) for l in lens])
+    exp = oracle_c.batch(arena, offs, lens)
+    bad = [3, 77, 499]
+    exp_t = exp.copy()
+    exp_t[bad] ^= 1
+    a = torch.from_numpy(arena).cuda()
+    o = torch.from_numpy(offs.astype(np.int64)).cuda()
+    l = torch.from_numpy(lens.astype(np.int32)).cuda()
+    e = torch.from_numpy(exp_t.view(np.int32)).cuda()
+    out = torch.zeros(500, dtype=torch.int32, device="cuda")
+    mism = torch.zeros(16, dtype=torch.int32, device="cuda")
+    cnt = torch.zeros(1, dtype=torch.int32, device="cuda")
+    dev.verify_device(a, o, l, e, out, mism, cnt)
+    torch.cuda.synchronize()
+    assert int(cnt.item()) == 3
+    assert sorted(mism[:3].cpu().tolist()) == bad
+    np.testing.assert_array_equal(out.cpu().numpy().view(np.uint32), exp)
+
+
+def test_host_buffer_api(dev, oracle_c):
+    arena = oracle.splitmix_bytes(1 << 20, 14)
+    rng = np.random.default_rng(14)
+    lens = rng.integers(0, 100_000, 64)
+    offs = np.array([rng.integers(0, (1 << 20) - l) for l in lens])
+    np.testing.assert_array_equal(dev.batch_host(arena, offs, lens), oracle_c.batch(arena, offs, lens))
+
+
+def test_set_path_256k_value(dev, oracle_c):
+    """C5: one 256 KiB value through the host-buffer entry (pinned staging)."""
+    buf = dev.PinnedBuffer(256 * 1024)
+    buf.array[:] = oracle.splitmix_bytes(256 * 1024, 15)
+    got = dev.batch_host(buf.array, [0], [256 * 1024])
+    assert got[0] == oracle_c.crc32(buf.array)
+    buf.free()
+
+
+def test_synth_device_matches_host(dev):
+    t = torch.empty(1 << 20 | 5, dtype=torch.uint8, device="cuda")
+    dev.synth_fill_device(t, 0xFEED)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(t.cpu().numpy(), oracle.splitmix_bytes(t.numel(), 0xFEED))
+
+
+def _digest(ref_crc, crcs: np.ndarray):
+    return {"count": len(crcs), "xor": f"{int(np.bitwise_xor.reduce(crcs)):08x}",
+            "crc_of_crcs": f"{ref_crc(crcs.astype('<u4').tobytes()):08x}"}
+
+
+def test_full_size_c2_digest(dev, oracle_c, digests):
+    """C2 at BASELINE size (1 Mi x 4 KiB = 4 GiB), bit-exact vs the digest of
+    the reference's own crcs."""
+    d = digests["C2"]
+    n = d["records"]
+    arena = torch.empty(n * 4096, dtype=torch.uint8, device="cuda")
+    dev.synth_fill_device(arena, d["seed"])
+    offs = torch.arange(n, dtype=torch.int64, device="cuda") * 4096
+    lens = torch.full((n,), 4096, dtype=torch.int32, device="cuda")
+    out = torch.empty(n, dtype=torch.int32, device="cuda")
+    dev.batch_device(arena, offs, lens, out)
+    torch.cuda.synchronize()
+    got = _digest(oracle_c.crc32, out.cpu().numpy().view(np.uint32))
+    assert got == {k: d[k] for k in ("count", "xor", "crc_of_crcs")}
+    del arena
+
+
+def test_full_size_c3_digest(dev, oracle_c, digests):
+    """C3 at BASELINE size (Zipf 64 B..1 MiB, ~4 GiB, any alignment)."""
+    d = digests["C3"]
+    lens = dev.zipf_lengths(d["target"], d["len_seed"])
+    assert len(lens) == d["count"] and int(lens.sum()) == d["total_bytes"]
+    offs = np.zeros(len(lens), np.int64)
+    offs[1:] = np.cumsum(lens[:-1].astype(np.int64))
+    arena = torch.empty(d["total_bytes"] + 64, dtype=torch.uint8, device="cuda")
+    dev.synth_fill_device(arena[: d["total_bytes"]], d["seed"])
+    out = torch.empty(len(lens), dtype=torch.int32, device="cuda")
+    dev.batch_device(arena, torch.from_numpy(offs).cuda(), torch.from_numpy(lens.view(np.int32)).cuda(),
+                     out)
+    torch.cuda.synchronize()
+    got = _digest(oracle_c.crc32, out.cpu().numpy().view(np.uint32))
+    assert got == {k: d[k] for k in ("count", "xor", "crc_of_crcs")}
+
+
+def test_repeat_is_deterministic(dev):
+    arena = oracle.splitmix_bytes(3 << 20, 16)
+    rng = np.random.default_rng(16)
+    lens = rng.integers(0, 1 << 20, 50)
+    offs = np.array([rng.integers(0, (3 << 20) - l) for l in lens])
+    a = gpu_batch(dev, arena, offs, lens)
+    for _ in range(3):
+        np.testing.assert_array_equal(gpu_batch(dev, arena, offs, lens), a)
+
+
+# ------------------------------------------------------ integrity tool ------
+
+TOOL_CASES = ["mixed", "zipf_small", "fixed_4k", "corrupt_payload", "corrupt_crc", "multi_errors",
+              "truncated_payload", "truncated_header", "bad_magic", "header_only"]
+
+
+@pytest.mark.parametrize("name", TOOL_CASES)
+def test_tool_gpu_engine_matches_reference(tmp_path, datafile_cases, name):
+    from test_tool_cpu import expected, run_tool
+    out, err, code = run_tool(name, tmp_path, "hip")
+    eout, eerr = expected(name)
+    assert out == eout
+    assert err == eerr
+    assert code == {c["name"]: c for c in datafile_cases}[name]["exit"]

@@ -1,0 +1,163 @@
+"""CPU tests of the product library's host side: the scalar drop-in engine,
+the GF(2) helpers, the C ABI surface, the datafile walk/encoders and the
+synthetic-input generators.  No GPU call is made here."""
+from __future__ import annotations
+
+import re
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+import oracle
+import zdbcrc
+from conftest import GOLDEN, ROOT, kat_bytes
+
+
+# ---------------------------------------------------------------- ABI -------
+
+def _declared_functions():
+    names = set()
+    for h in (ROOT / "include").glob("*.h"):
+        text = re.sub(r"/\*.*?\*/", "", h.read_text(), flags=re.S)
+        for m in re.finditer(r"^[A-Za-z_][\w\s\*]*?\b(zdb_\w+)\s*\(", text, flags=re.M):
+            names.add(m.group(1))
+    return names
+
+
+def test_every_declared_symbol_is_exported():
+    declared = _declared_functions()
+    assert len(declared) >= 20
+    assert declared == set(zdbcrc.EXPORTED)
+    for name in declared:
+        assert hasattr(zdbcrc._lib, name), name
+
+
+def test_scalar_path_never_touches_hip():
+    # key hashing / CHECK must not initialise the GPU (fork safety)
+    code = ("import sys; sys.path.insert(0, %r); import zdbcrc; "
+            "zdbcrc.crc32(b'k'*255); zdbcrc.checksum_crc32(b'x'*4096); zdbcrc.shift(1, 100); "
+            "zdbcrc.datafile_walk(open(%r,'rb').read()); "
+            "print(zdbcrc.gpu_initialized(), zdbcrc.batch_engine())"
+            % (str(ROOT / "0-db_amd"), str(GOLDEN / "datafiles" / "mixed.d0")))
+    out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, check=True)
+    assert out.stdout.split() == ["False", "uninitialized"]
+
+
+# ------------------------------------------------------- scalar engine ------
+
+def test_engine_value():
+    assert zdbcrc.engine_value() == "sse42"
+
+
+def test_scalar_known_answers(kats):
+    for e in kats:
+        data = kat_bytes(e)
+        assert zdbcrc.crc32(data) == int(e["crc"], 16), e["name"]
+        assert zdbcrc.checksum_crc32(data) == int(e["crc"], 16), e["name"]
+
+
+def test_scalar_vectors_all_alignments(vectors):
+    lens, seeds, crcs = vectors
+    for n, s, c in zip(lens, seeds, crcs):
+        if n > 70_000:
+            continue
+        buf = np.zeros(int(n) + 16, dtype=np.uint8)
+        data = oracle.splitmix_bytes(int(n), int(s))
+        for mis in (0, 1, 7, 13):
+            buf[mis:mis + n] = data
+            assert zdbcrc.crc32(buf[mis:mis + n]) == int(c)
+
+
+def test_negative_length_is_zero():
+    assert zdbcrc._crc32(None, -5) == 0
+
+
+# ----------------------------------------------------------- GF(2) ----------
+
+def test_combine_and_shift(oracle_c):
+    rng = np.random.default_rng(3)
+    for _ in range(200):
+        a = oracle.splitmix_bytes(int(rng.integers(0, 3000)), int(rng.integers(1 << 30)))
+        b = oracle.splitmix_bytes(int(rng.integers(0, 3000)), int(rng.integers(1 << 30)))
+        ca, cb = oracle_c.crc32(a), oracle_c.crc32(b)
+        assert zdbcrc.combine(ca, cb, len(b)) == oracle_c.crc32(np.concatenate([a, b]))
+        n = int(rng.integers(-100_000, 100_000))
+        assert zdbcrc.shift(zdbcrc.shift(ca, n), -n) == ca
+        # shift over n zero bytes == crc of data followed by n zeros
+        k = int(rng.integers(0, 500))
+        assert zdbcrc.shift(ca, k) == oracle_c.crc32(np.concatenate([a, np.zeros(k, np.uint8)]))
+
+
+def test_zero_prefix_invariance(oracle_c):
+    d = oracle.splitmix_bytes(777, 1)
+    assert oracle_c.crc32(np.concatenate([np.zeros(333, np.uint8), d])) == oracle_c.crc32(d)
+
+
+def test_large_shift_matches_repeated():
+    c = 0x12345678
+    x = c
+    for _ in range(16):
+        x = zdbcrc.shift(x, 1 << 20)
+    assert zdbcrc.shift(c, 16 << 20) == x
+
+
+# --------------------------------------------------------- synthetic --------
+
+@pytest.mark.parametrize("n", [0, 1, 7, 8, 9, 63, 64, 65, 1000, 4097, 1 << 20])
+def test_synth_matches_restatement(n):
+    np.testing.assert_array_equal(zdbcrc.synth_fill(n, 0xABC + n), oracle.splitmix_bytes(n, 0xABC + n))
+
+
+def test_zipf_recipe():
+    lens = zdbcrc.zipf_lengths(256 << 20, 0xC3C3C3)
+    assert lens.min() >= 64 and lens.max() <= 1 << 20
+    assert lens.sum() >= 256 << 20
+    # ~78 % of records <= 4 KiB, ~79 % of bytes in records >= 256 KiB
+    assert 0.70 < (lens <= 4096).mean() < 0.85
+    big = lens[lens >= 256 * 1024].sum() / lens.sum()
+    assert 0.70 < big < 0.88
+    np.testing.assert_array_equal(lens, zdbcrc.zipf_lengths(256 << 20, 0xC3C3C3))
+
+
+# ---------------------------------------------------------- datafile --------
+
+@pytest.mark.parametrize("name", ["mixed", "zipf_small", "fixed_4k", "corrupt_payload",
+                                  "truncated_payload", "truncated_header", "bad_magic",
+                                  "bad_version", "header_only"])
+def test_walk_matches_oracle_scan(oracle_c, name):
+    img = (GOLDEN / "datafiles" / f"{name}.d0").read_bytes()
+    recs, status = zdbcrc.datafile_walk(img)
+    orecs, _, fatal = oracle_c.integrity_scan(img)
+    assert status == fatal
+    assert len(recs) == len(orecs)
+    for f in ("header_offset", "payload_offset", "datalength", "integrity", "previous", "idlength",
+              "flags"):
+        np.testing.assert_array_equal(recs[f].astype(np.uint64), orecs[f].astype(np.uint64), f)
+
+
+def test_reencode_is_byte_identical():
+    """Encoding every walked record back (header + key + payload) reproduces
+    the reference-written datafile byte for byte (data.c:594-633 framing)."""
+    img = (GOLDEN / "datafiles" / "mixed.d0").read_bytes()
+    recs, status = zdbcrc.datafile_walk(img)
+    assert status == 0
+    out = bytearray(img[:28])
+    assert zdbcrc.encode_header(0)[:8] == img[:8]
+    for r in recs:
+        h = int(r["header_offset"])
+        key = img[h + 18:h + 18 + int(r["idlength"])]
+        out += zdbcrc.encode_entry(key, int(r["datalength"]), int(r["previous"]), int(r["integrity"]),
+                                   int(r["flags"]), int(r["timestamp"]))
+        p = int(r["payload_offset"])
+        out += img[p:p + int(r["datalength"])]
+    assert bytes(out) == img
+
+
+def test_deleted_entries_present():
+    img = (GOLDEN / "datafiles" / "mixed.d0").read_bytes()
+    recs, _ = zdbcrc.datafile_walk(img)
+    deleted = recs[recs["flags"] & 1 == 1]
+    assert len(deleted) == 2
+    assert (deleted["datalength"] == 0).all() and (deleted["integrity"] == 0).all()

@@ -1,0 +1,63 @@
+"""The kernel's algorithm, replayed on the CPU (tests/kernel_model.py) with
+the library's real table image, against the oracle.  Covers the math of
+crc32_hip.hip -- lane mapping, supersteps, edge masks, trailing-pad removal,
+segment splits across waves and the atomic-XOR recombination -- without a
+GPU.  The GPU tests check the HIP implementation of the same algorithm."""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+
+import kernel_model as km
+import oracle
+import zdbcrc
+
+
+@pytest.fixture(scope="module")
+def tab():
+    t = zdbcrc.table_image()
+    assert len(t) == km.TABLE_DW
+    return t
+
+
+def _case(seed, nrec, maxlen, arena_len):
+    rng = np.random.default_rng(seed)
+    arena = oracle.splitmix_bytes(arena_len, seed)
+    lens = rng.integers(0, maxlen + 1, nrec)
+    offs = np.array([rng.integers(0, arena_len - l + 1) for l in lens])
+    return arena, offs, lens
+
+
+def test_table_spot_values(tab):
+    # slot K-1 of the data tables is plain crc of a piece with one slice set
+    piece = np.zeros(16, np.uint8)
+    piece[0] = 1
+    assert tab[km.OFF_T + ((km.K - 1) * km.PCH + 0) * 32 + 1] == oracle.crc32_py(piece.tobytes())
+    # lane 63 is not shifted at all
+    for v in range(32):
+        assert tab[km.OFF_L + (0 * 32 + v) * 64 + 63] == v
+
+
+@pytest.mark.parametrize("base", [0, 5, 15])
+def test_edges_and_small(oracle_c, tab, base):
+    arena = oracle.splitmix_bytes(5000, 11)
+    lens = [0, 1, 2, 3, 4, 5, 8, 15, 16, 17, 20, 31, 32, 33, 47, 48, 49, 63, 64, 65]
+    offs = [(7 * i) % 3000 for i in range(len(lens))]
+    got = km.batch(arena, offs, lens, tab, base_addr=base)
+    np.testing.assert_array_equal(got, oracle_c.batch(arena, offs, lens))
+
+
+@pytest.mark.parametrize("max_waves,min_units", [(4096, 256), (5, 16), (11, 1), (2, 1)])
+def test_random_split_geometries(oracle_c, tab, max_waves, min_units):
+    arena, offs, lens = _case(max_waves * 7 + min_units, 24, 9000, 60_000)
+    got = km.batch(arena, offs, lens, tab, max_waves=max_waves, min_units=min_units, base_addr=3)
+    np.testing.assert_array_equal(got, oracle_c.batch(arena, offs, lens))
+
+
+def test_multi_superstep_record(oracle_c, tab):
+    # > K KiB so the register is advanced across supersteps; split 3 ways
+    arena = oracle.splitmix_bytes(40_000, 21)
+    offs, lens = [13, 100], [33_333, 5_000]
+    for mw, mu in ((4096, 256), (3, 1)):
+        got = km.batch(arena, offs, lens, tab, max_waves=mw, min_units=mu)
+        np.testing.assert_array_equal(got, oracle_c.batch(arena, offs, lens))
