@@ -29,8 +29,14 @@
  *     libc call left (in practice the localtime() zone lookup), SURVEY App.A.6;
  *   - exit status = number of mismatches (:162-165), reported as
  *     "[-] data file inconsistency: %d error(s)".
+ *
+ * Linking: the header walk and the scalar engine are linked in statically;
+ * libzdbcrc.so (HIP) is dlopen'ed only when the GPU engine is about to run,
+ * after the header report, so the HIP runtime's own start-up (which touches
+ * the time-zone state) happens where the reference's process does nothing.
  */
 #define _GNU_SOURCE
+#include <dlfcn.h>
 #include <errno.h>
 #include <fcntl.h>
 #include <libgen.h>
@@ -126,9 +132,42 @@ static void ob_flush(outbuf_t *b) {
     b->n = 0;
 }
 
+/* ---- GPU engine, resolved at run time ------------------------------------ */
+
+typedef struct {
+    int (*batch)(const uint8_t *, size_t, const uint64_t *, const uint32_t *, uint32_t *, size_t);
+    const char *(*strerror)(int);
+    void *(*host_alloc)(size_t);
+} gpu_api_t;
+
+static int load_gpu(gpu_api_t *api) {
+    const char *env = getenv("ZDBCRC_LIB");
+    char path[4096];
+    if (env) {
+        snprintf(path, sizeof(path), "%s", env);
+    } else {
+        char exe[4096];
+        ssize_t n = readlink("/proc/self/exe", exe, sizeof(exe) - 1);
+        if (n <= 0)
+            return -1;
+        exe[n] = 0;
+        snprintf(path, sizeof(path), "%s/../lib/libzdbcrc.so", dirname(exe));
+    }
+    void *h = dlopen(path, RTLD_NOW | RTLD_LOCAL);
+    if (!h) {
+        fprintf(stderr, "[-] zdb-integrity-check: cannot load %s: %s\n", path, dlerror());
+        return -1;
+    }
+    api->batch = (int (*)(const uint8_t *, size_t, const uint64_t *, const uint32_t *, uint32_t *,
+                          size_t))dlsym(h, "zdb_crc32_batch");
+    api->strerror = (const char *(*)(int))dlsym(h, "zdb_crc32_strerror");
+    api->host_alloc = (void *(*)(size_t))dlsym(h, "zdb_crc32_host_alloc");
+    return (api->batch && api->strerror && api->host_alloc) ? 0 : -1;
+}
+
 /* ---- file loading --------------------------------------------------------- */
 
-static uint8_t *load_file(int fd, size_t *len, int pinned, int *read_errno) {
+static uint8_t *load_file(int fd, size_t *len, const gpu_api_t *gpu, int *read_errno) {
     struct stat sb;
     *read_errno = 0;
     if (fstat(fd, &sb) != 0) {
@@ -136,7 +175,7 @@ static uint8_t *load_file(int fd, size_t *len, int pinned, int *read_errno) {
         return NULL;
     }
     size_t size = (size_t)sb.st_size;
-    uint8_t *buf = pinned ? zdb_crc32_host_alloc(size + 16) : malloc(size + 16);
+    uint8_t *buf = gpu ? gpu->host_alloc(size + 16) : malloc(size + 16);
     if (!buf) {
         *read_errno = ENOMEM;
         return NULL;
@@ -211,24 +250,18 @@ int main(int argc, char *argv[]) {
         return errors;
     }
 
-    size_t len = 0;
-    int read_errno = 0;
-    uint8_t *image = load_file(fd, &len, use_gpu, &read_errno);
-    close(fd);
-    if (!image) {
-        warnp(path, read_errno);
-        return EXIT_FAILURE;
-    }
-
-    /* descriptor load + validate (data.c:177-209) */
-    if (len < ZDB_DATA_HEADER_SIZE) {
+    /* descriptor load + validate (data.c:177-209), before anything touches
+     * the GPU so that errno evolves as in the reference process */
+    uint8_t hdr[ZDB_DATA_HEADER_SIZE];
+    if (pread(fd, hdr, sizeof(hdr), 0) != (ssize_t)sizeof(hdr)) {
+        close(fd);
         fflush(stdout);
         fprintf(stderr, "[-] data file inconsistency: %d error(s)\n", 1);
         return 1;
     }
     uint32_t version;
-    memcpy(&version, image + 4, 4);
-    if (memcmp(image, "DAT0", 4)) {
+    memcpy(&version, hdr + 4, 4);
+    if (memcmp(hdr, "DAT0", 4)) {
         timelog(stdout);
         printf(COLOR_RED "[-] %s: invalid header, wrong magic" COLOR_RESET "\n", path);
         fflush(stdout);
@@ -247,11 +280,12 @@ int main(int argc, char *argv[]) {
     }
 
     uint64_t created, opened;
-    memcpy(&created, image + 8, 8);
-    memcpy(&opened, image + 16, 8);
+    memcpy(&created, hdr + 8, 8);
+    memcpy(&opened, hdr + 16, 8);
     char datestr[64];
     printf("[+] integrity-check: header seems correct\n");
     /* zdb_header_date takes a uint32_t epoch (libzdb.c:156) */
+    errno = 0;
     time_t t = (time_t)(uint32_t)created;
     strftime(datestr, sizeof(datestr), "%F %T", localtime(&t));
     printf("[+] integrity-check: created at: %s\n", datestr);
@@ -259,6 +293,22 @@ int main(int argc, char *argv[]) {
     strftime(datestr, sizeof(datestr), "%F %T", localtime(&t));
     printf("[+] integrity-check: last open: %s\n", datestr);
     const int stale_errno = errno; /* what zdb_diep would report below */
+
+    gpu_api_t gpu = {0};
+    if (use_gpu && load_gpu(&gpu) != 0) {
+        fflush(stdout);
+        fprintf(stderr, "[-] zdb-integrity-check: GPU engine unavailable (use --engine=cpu)\n");
+        return EXIT_FAILURE;
+    }
+
+    size_t len = 0;
+    int read_errno = 0;
+    uint8_t *image = load_file(fd, &len, use_gpu ? &gpu : NULL, &read_errno);
+    close(fd);
+    if (!image) {
+        warnp(path, read_errno);
+        return EXIT_FAILURE;
+    }
 
     /* header walk -> descriptors */
     int status = 0;
@@ -275,11 +325,11 @@ int main(int argc, char *argv[]) {
     size_t m = zdb_datafile_payloads(recs, (size_t)nfull, offs, lens, NULL, idx);
     if (m) {
         if (use_gpu) {
-            int rc = zdb_crc32_batch(image, len, offs, lens, crc, m);
+            int rc = gpu.batch(image, len, offs, lens, crc, m);
             if (rc) {
                 fflush(stdout);
                 fprintf(stderr, "[-] zdb-integrity-check: GPU engine failed: %s (use --engine=cpu)\n",
-                        zdb_crc32_strerror(rc));
+                        gpu.strerror(rc));
                 return EXIT_FAILURE;
             }
         } else {
