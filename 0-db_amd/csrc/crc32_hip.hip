@@ -35,6 +35,7 @@
 //    one inverse shift x^(-8z) on the scalar unit).
 
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <mutex>
@@ -53,8 +54,6 @@ namespace {
 constexpr int K = ZDBCRC_K;
 constexpr int PCH = ZDBCRC_PCH;
 constexpr int SCH = ZDBCRC_SCH;
-constexpr int WG_THREADS = 512;
-constexpr int WAVES_PER_WG = WG_THREADS / 64;
 constexpr int WG_PER_CU = 2;              // 2 x 70 KiB of LDS tables per CU
 constexpr uint64_t UNIT_OVH = 16;         // planning charge per record, in pieces
 constexpr uint64_t MIN_UNITS_PER_WAVE = 256;
@@ -79,13 +78,19 @@ __device__ __forceinline__ uint32_t piece_slice(const uint4 &v, int c) {
     return __builtin_amdgcn_alignbit(word_of(v, d + 1), word_of(v, d), sh) & 31u;
 }
 
-// contribution of one piece in slot I of a superstep
+// contribution of one piece in slot I of a superstep: 26 conflict-free
+// lookups, folded three at a time (v_bitop3 xor3) in issue order
 template <int I>
 __device__ __forceinline__ uint32_t piece_contrib(const uint4 &v, const uint32_t *lds) {
-    uint32_t r = 0;
+    const uint32_t *tab = lds + ZDBCRC_OFF_T + I * PCH * 32;
+    uint32_t r = tab[(PCH - 2) * 32 + piece_slice(v, PCH - 2)] ^ tab[(PCH - 1) * 32 + piece_slice(v, PCH - 1)];
 #pragma unroll
-    for (int c = 0; c < PCH; c++)
-        r ^= lds[ZDBCRC_OFF_T + (I * PCH + c) * 32 + piece_slice(v, c)];
+    for (int c = 0; c + 2 < PCH; c += 3) {
+        const uint32_t a = tab[c * 32 + piece_slice(v, c)];
+        const uint32_t b = tab[(c + 1) * 32 + piece_slice(v, c + 1)];
+        const uint32_t d = tab[(c + 2) * 32 + piece_slice(v, c + 2)];
+        r = r ^ a ^ b ^ d;
+    }
     return r;
 }
 
@@ -151,12 +156,22 @@ struct SegCtx {
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef const __attribute__((address_space(1))) u32x4 global_u32x4;
 
+// piece for step t on this lane; CHECK: lanes before the segment start read
+// nothing (only the first superstep has such lanes)
+template <bool CHECK>
 __device__ __forceinline__ uint4 load_piece(const SegCtx &s, uint32_t t, uint32_t lane) {
     const int64_t jj = s.base_j + 64 * (int64_t)t + (int64_t)lane;
     u32x4 v = {0, 0, 0, 0};
-    if (jj >= (int64_t)s.pa)
+    if (!CHECK || jj >= (int64_t)s.pa)
         v = *reinterpret_cast<global_u32x4 *>(s.P0 + 16u * (uint64_t)jj);
     return make_uint4(v.x, v.y, v.z, v.w);
+}
+
+template <bool CHECK>
+__device__ __forceinline__ void load_superstep(const SegCtx &s, uint32_t ss, uint32_t lane, uint4 (&buf)[K]) {
+#pragma unroll
+    for (int i = 0; i < K; i++)
+        buf[i] = load_piece<CHECK>(s, ss * K + i, lane);
 }
 
 // zero the bytes of a piece that lie outside the record (first/last piece only)
@@ -168,7 +183,30 @@ __device__ __forceinline__ uint4 fix_edges(const SegCtx &s, uint4 v, uint32_t t,
     return v;
 }
 
-// CRC (in padded-record space) of pieces [pa, pb) of one record, wave-reduced
+// one superstep (K steps) folded into the lane register.  Only the first
+// superstep can hold empty leading steps / lanes and the record's first
+// piece; only the last can hold the record's last piece: EDGE enables the
+// checks there, the middle supersteps run without them.
+template <bool EDGE>
+__device__ __forceinline__ uint32_t superstep(const SegCtx &s, uint32_t acc, const uint4 (&cur)[K], uint32_t ss,
+                                              uint32_t t0, uint32_t lane, const uint32_t *lds) {
+    if (ss)
+        acc = advance_superstep(acc, lds);
+    const uint32_t tb = ss * K;
+#define ZDBCRC_SLOT(I)                                                                   \
+    if (tb + I >= t0)                                                                    \
+        acc ^= piece_contrib<I>(EDGE ? fix_edges(s, cur[I], tb + I, lane) : cur[I], lds);
+
+    ZDBCRC_SLOT(0)
+    ZDBCRC_SLOT(1)
+    ZDBCRC_SLOT(2)
+    ZDBCRC_SLOT(3)
+#undef ZDBCRC_SLOT
+    return acc;
+}
+
+// CRC (in padded-record space) of pieces [pa, pb) of one record, wave-reduced.
+// Loads run one superstep (4 KiB per wave) ahead of the lookups.
 __device__ __forceinline__ uint32_t segment_crc(const SegCtx &s, uint32_t pb, uint32_t lane,
                                                 const uint32_t *lds) {
     const uint32_t nps = pb - s.pa;
@@ -177,38 +215,29 @@ __device__ __forceinline__ uint32_t segment_crc(const SegCtx &s, uint32_t pb, ui
     const uint32_t t0 = S * K - T; // first step holding any piece of the segment
 
     uint32_t acc = 0;
-    uint4 cur[K];
+    uint4 cur[K], nxt[K];
+    load_superstep<true>(s, 0, lane, cur);
+    if (S == 1)
+        return wave_xor(lane_place(superstep<true>(s, acc, cur, 0, t0, lane, lds), lane, lds));
+    load_superstep<false>(s, 1, lane, nxt);
+    acc = superstep<true>(s, acc, cur, 0, t0, lane, lds);
+    uint32_t ss = 1;
+    for (; ss + 1 < S; ss++) {
 #pragma unroll
-    for (int i = 0; i < K; i++)
-        cur[i] = load_piece(s, i, lane);
-
-    for (uint32_t ss = 0; ss < S; ss++) {
-        uint4 nxt[K];
-        const bool more = ss + 1 < S;
-        if (more) {
-#pragma unroll
-            for (int i = 0; i < K; i++)
-                nxt[i] = load_piece(s, (ss + 1) * K + i, lane);
-        }
-        if (ss)
-            acc = advance_superstep(acc, lds);
-        const uint32_t tb = ss * K;
-        if (tb + 0 >= t0) acc ^= piece_contrib<0>(fix_edges(s, cur[0], tb + 0, lane), lds);
-        if (tb + 1 >= t0) acc ^= piece_contrib<1>(fix_edges(s, cur[1], tb + 1, lane), lds);
-        if (tb + 2 >= t0) acc ^= piece_contrib<2>(fix_edges(s, cur[2], tb + 2, lane), lds);
-        if (tb + 3 >= t0) acc ^= piece_contrib<3>(fix_edges(s, cur[3], tb + 3, lane), lds);
-        if (more) {
-#pragma unroll
-            for (int i = 0; i < K; i++)
-                cur[i] = nxt[i];
-        }
+        for (int i = 0; i < K; i++)
+            cur[i] = nxt[i];
+        load_superstep<false>(s, ss + 1, lane, nxt);
+        acc = superstep<false>(s, acc, cur, ss, t0, lane, lds);
     }
+    acc = superstep<true>(s, acc, nxt, ss, t0, lane, lds);
     return wave_xor(lane_place(acc, lane, lds));
 }
 
 static_assert(K == 4, "segment_crc unrolls 4 slots");
 
-__global__ __launch_bounds__(WG_THREADS, 4) void crc_batch_kernel(
+// WGT threads per workgroup, WPE = minimum waves per SIMD (register budget)
+template <int WGT, int WPE>
+__global__ __launch_bounds__(WGT, WPE) void crc_batch_kernel(
     const uint8_t *__restrict__ arena, const uint64_t *__restrict__ offsets,
     const uint32_t *__restrict__ lengths, const uint64_t *__restrict__ unit_start, uint64_t n,
     uint32_t *__restrict__ out, const uint32_t *__restrict__ tables, uint32_t max_waves) {
@@ -217,13 +246,13 @@ __global__ __launch_bounds__(WG_THREADS, 4) void crc_batch_kernel(
     {
         const uint4 *src = reinterpret_cast<const uint4 *>(tables);
         uint4 *dst = reinterpret_cast<uint4 *>(lds);
-        for (int i = threadIdx.x; i < ZDBCRC_LDS_DW / 4; i += WG_THREADS)
+        for (int i = threadIdx.x; i < ZDBCRC_LDS_DW / 4; i += WGT)
             dst[i] = src[i];
     }
     __syncthreads();
 
     const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t gw = __builtin_amdgcn_readfirstlane(blockIdx.x * WAVES_PER_WG + (threadIdx.x >> 6));
+    const uint32_t gw = __builtin_amdgcn_readfirstlane(blockIdx.x * (WGT / 64) + (threadIdx.x >> 6));
     const uint64_t total = unit_start[n];
     uint64_t nwaves = (total + MIN_UNITS_PER_WAVE - 1) / MIN_UNITS_PER_WAVE;
     if (nwaves > max_waves)
@@ -290,6 +319,34 @@ __global__ __launch_bounds__(WG_THREADS, 4) void crc_batch_kernel(
         if (ur >= ue || r + 1 >= n)
             break;
     }
+}
+
+typedef void (*crc_kernel_fn)(const uint8_t *, const uint64_t *, const uint32_t *, const uint64_t *, uint64_t,
+                              uint32_t *, const uint32_t *, uint32_t);
+
+struct KernelVariant {
+    const char *name;
+    crc_kernel_fn fn;
+    int threads;
+};
+
+// selectable with ZDBCRC_VARIANT=<index> (A/B measurement); 0 is the default
+const KernelVariant kVariants[] = {
+    {"wg512_w4", crc_batch_kernel<512, 4>, 512},
+    {"wg768_w6", crc_batch_kernel<768, 6>, 768},
+    {"wg1024_w4", crc_batch_kernel<1024, 4>, 1024},
+};
+
+constexpr int kNumVariants = (int)(sizeof(kVariants) / sizeof(kVariants[0]));
+int g_variant = -1;
+
+const KernelVariant &variant() {
+    if (g_variant < 0) {
+        const char *e = std::getenv("ZDBCRC_VARIANT");
+        int i = e ? std::atoi(e) : 0;
+        g_variant = (i >= 0 && i < kNumVariants) ? i : 0;
+    }
+    return kVariants[g_variant];
 }
 
 // unit count per record: UNIT_OVH + number of 16-byte pieces it touches
@@ -443,8 +500,9 @@ int enqueue_batch(DeviceCtx &c, const uint8_t *arena, const uint64_t *offsets, c
                                 rocprim::plus<uint64_t>(), st) != hipSuccess)
         return ZDB_CRC32_ELAUNCH;
 
+    const KernelVariant &kv = variant();
     const uint32_t grid = (uint32_t)(c.cus * WG_PER_CU);
-    const uint32_t max_waves = grid * WAVES_PER_WG;
+    const uint32_t max_waves = grid * (uint32_t)(kv.threads / 64);
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (g_timing) {
         for (hipEvent_t *e : {&e0, &e1}) {
@@ -457,8 +515,8 @@ int enqueue_batch(DeviceCtx &c, const uint8_t *arena, const uint64_t *offsets, c
         }
         hipEventRecord(e0, st);
     }
-    hipLaunchKernelGGL(crc_batch_kernel, dim3(grid), dim3(WG_THREADS), 0, st, arena, offsets, lengths,
-                       unit_start, n, out, c.d_tables, max_waves);
+    hipLaunchKernelGGL(kv.fn, dim3(grid), dim3(kv.threads), 0, st, arena, offsets, lengths, unit_start, n,
+                       out, c.d_tables, max_waves);
     if (hipGetLastError() != hipSuccess)
         return ZDB_CRC32_ELAUNCH;
     if (g_timing) {
@@ -503,6 +561,16 @@ const char *zdb_crc32_batch_engine(void) {
 }
 
 int zdb_crc32_gpu_initialized(void) { return g_hip_touched ? 1 : 0; }
+
+// measurement hook (not part of the public ABI): select a kernel variant for
+// A/B timing in one process; returns its name, NULL if out of range
+const char *zdbcrc_debug_set_variant(int idx) {
+    std::lock_guard<std::mutex> g(g_mu);
+    if (idx < 0 || idx >= kNumVariants)
+        return nullptr;
+    g_variant = idx;
+    return kVariants[idx].name;
+}
 
 int zdb_crc32_batch_device(const uint8_t *d_arena, const uint64_t *d_offsets, const uint32_t *d_lengths,
                            uint32_t *d_out, size_t n, void *stream) {

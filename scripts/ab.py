@@ -1,0 +1,58 @@
+#!/usr/bin/env python3
+"""Interleaved A/B of kernel variants in ONE process (rule 24): for each
+round, every variant runs STEPS batches of the same device-resident dataset;
+reports median/min kernel ms per variant and checks each variant's output
+against variant 0 bit for bit."""
+import ctypes as C, json, sys, time
+from pathlib import Path
+import numpy as np
+ROOT = Path(__file__).resolve().parents[1]
+sys.path[:0] = [str(ROOT / "0-db_amd")]
+import torch, zdbcrc
+
+set_variant = zdbcrc._lib.zdbcrc_debug_set_variant
+set_variant.restype = C.c_char_p
+set_variant.argtypes = [C.c_int]
+names = []
+i = 0
+while True:
+    n = set_variant(i)
+    if not n:
+        break
+    names.append(n.decode()); i += 1
+sel = [int(x) for x in sys.argv[2].split(",")] if len(sys.argv) > 2 else list(range(len(names)))
+work = sys.argv[1] if len(sys.argv) > 1 else "zipf"
+ROUNDS, STEPS = 5, 5
+for wl in work.split(","):
+    if wl == "zipf":
+        lens = zdbcrc.zipf_lengths(4 << 30, 0xC3C3C3).astype(np.int64)
+        seed = 0x5A0DB5EED + 3
+    else:
+        lens = np.full(1 << 20, 4096, np.int64); seed = 0x5A0DB5EED
+    offs = np.zeros(len(lens), np.int64); offs[1:] = np.cumsum(lens[:-1])
+    total = int(offs[-1] + lens[-1])
+    arena = torch.empty(total + 64, dtype=torch.uint8, device="cuda")
+    zdbcrc.synth_fill_device(arena, seed)
+    do, dl = torch.from_numpy(offs).cuda(), torch.from_numpy(lens.astype(np.int32)).cuda()
+    outs = {v: torch.empty(len(lens), dtype=torch.int32, device="cuda") for v in sel}
+    times = {v: [] for v in sel}
+    for r in range(ROUNDS):
+        for v in sel:
+            set_variant(v)
+            zdbcrc.batch_device(arena, do, dl, outs[v])
+            torch.cuda.synchronize(); zdbcrc.kernel_stats(); zdbcrc.set_timing(True)
+            for _ in range(STEPS):
+                zdbcrc.batch_device(arena, do, dl, outs[v])
+            torch.cuda.synchronize(); zdbcrc.set_timing(False)
+            ms, k = zdbcrc.kernel_stats(); times[v].append(ms / k)
+    ref = outs[sel[0]].cpu()
+    payload = int(lens.sum())
+    for v in sel:
+        t = np.array(times[v])
+        same = bool(torch.equal(outs[v].cpu(), ref))
+        print(json.dumps({"workload": wl, "variant": names[v], "median_ms": round(float(np.median(t)), 4),
+                          "min_ms": round(float(t.min()), 4),
+                          "gibs_median": round(payload / (np.median(t) / 1e3) / 2**30, 1),
+                          "frac_spec": round((payload + 16 * len(lens)) / (np.median(t) / 1e3) / 8e12, 4),
+                          "same_as_first": same}), flush=True)
+    del arena
