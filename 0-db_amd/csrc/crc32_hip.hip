@@ -235,8 +235,75 @@ __device__ __forceinline__ uint32_t segment_crc(const SegCtx &s, uint32_t pb, ui
 
 static_assert(K == 4, "segment_crc unrolls 4 slots");
 
-// WGT threads per workgroup, WPE = minimum waves per SIMD (register budget)
-template <int WGT, int WPE>
+// A record segment as the wave walks it (all fields wave-uniform).
+struct Seg {
+    SegCtx c;
+    uint64_t r;    // record index
+    uint32_t pb;   // one past the segment's last piece (record-relative)
+    uint32_t S;    // supersteps in the segment
+    uint32_t t0;   // first non-empty step
+    uint32_t z;    // zero bytes padding the record's last piece
+};
+
+// Next record segment of this wave's unit slice [ub, ue), starting at record
+// r (advanced past it).  False when the slice is exhausted.
+__device__ __forceinline__ bool next_seg(uint64_t &r, uint64_t n, uint64_t ub, uint64_t ue,
+                                         const uint64_t *__restrict__ unit_start, const uint8_t *arena,
+                                         const uint64_t *__restrict__ offsets,
+                                         const uint32_t *__restrict__ lengths, Seg &sg) {
+    for (;;) {
+        if (r >= n)
+            return false;
+        const uint64_t u0 = unit_start[r];
+        if (u0 >= ue)
+            return false;
+        const uint64_t us = u0 + UNIT_OVH;
+        const uint64_t ur = unit_start[r + 1];
+        const uint64_t s_lo = ub > us ? ub : us;
+        const uint64_t s_hi = ue < ur ? ue : ur;
+        if (s_hi > s_lo) {
+            const uint64_t A = reinterpret_cast<uint64_t>(arena) + offsets[r];
+            const uint64_t Aend = A + lengths[r];
+            sg.r = r;
+            sg.c.P0 = A & ~15ull;
+            sg.c.np = (uint32_t)(ur - us);
+            sg.z = (uint32_t)(sg.c.P0 + 16u * (uint64_t)sg.c.np - Aend);
+            sg.c.lo0 = (int)(A & 15u);
+            sg.c.hi_last = 16 - (int)sg.z;
+            sg.c.pa = (uint32_t)(s_lo - us);
+            sg.pb = (uint32_t)(s_hi - us);
+            const uint32_t T = (sg.pb - sg.c.pa + 63u) / 64u;
+            sg.S = (T + K - 1) / K;
+            sg.t0 = sg.S * K - T;
+            sg.c.base_j = (int64_t)sg.pb - 64 * (int64_t)sg.S * K;
+            r++;
+            return true;
+        }
+        r++;
+    }
+}
+
+// lane registers -> record contribution -> out[r]
+__device__ __forceinline__ void finish_seg(const Seg &sg, uint32_t acc, uint32_t lane, const uint32_t *lds,
+                                           const uint32_t *__restrict__ tables, uint32_t *__restrict__ out) {
+    uint32_t x = __builtin_amdgcn_readfirstlane(wave_xor(lane_place(acc, lane, lds)));
+    if (sg.z) // remove the zero bytes that pad the record's last piece
+        x = uniform_shift(x, tables + ZDBCRC_OFF_Z + sg.z * SCH * 32);
+    uint64_t q = sg.c.np - sg.pb; // record pieces after this segment
+    for (int g = 0; q; g++, q >>= 1)
+        if (q & 1)
+            x = uniform_shift(x, tables + ZDBCRC_OFF_G + g * SCH * 32);
+    if (lane == 0) {
+        if (sg.c.pa == 0 && sg.pb == sg.c.np)
+            out[sg.r] = x;
+        else
+            atomicXor(&out[sg.r], x);
+    }
+}
+
+// WGT threads per workgroup, WPE = minimum waves per SIMD (register budget),
+// PIPE: loads run one superstep ahead across record boundaries too
+template <int WGT, int WPE, bool PIPE>
 __global__ __launch_bounds__(WGT, WPE) void crc_batch_kernel(
     const uint8_t *__restrict__ arena, const uint64_t *__restrict__ offsets,
     const uint32_t *__restrict__ lengths, const uint64_t *__restrict__ unit_start, uint64_t n,
@@ -272,6 +339,46 @@ __global__ __launch_bounds__(WGT, WPE) void crc_batch_kernel(
             lo = mid;
         else
             hi = mid;
+    }
+
+    if (PIPE) {
+        // one stream of supersteps over all of the slice's segments; the next
+        // superstep's loads (possibly of the next record) are in flight while
+        // the current one is folded
+        uint64_t rn = lo;
+        Seg cur, nx;
+        if (!next_seg(rn, n, ub, ue, unit_start, arena, offsets, lengths, cur))
+            return;
+        uint32_t css = 0, acc = 0;
+        uint4 bufA[K], bufB[K];
+        load_superstep<true>(cur.c, 0, lane, bufA);
+        auto step = [&](const uint4(&X)[K], uint4(&Y)[K]) -> bool {
+            uint32_t nss = 0;
+            bool have = true;
+            if (css + 1 < cur.S) {
+                nx = cur;
+                nss = css + 1;
+                load_superstep<false>(nx.c, nss, lane, Y);
+            } else {
+                have = next_seg(rn, n, ub, ue, unit_start, arena, offsets, lengths, nx);
+                if (have)
+                    load_superstep<true>(nx.c, 0, lane, Y);
+            }
+            if (css == 0 || css + 1 == cur.S)
+                acc = superstep<true>(cur.c, acc, X, css, cur.t0, lane, lds);
+            else
+                acc = superstep<false>(cur.c, acc, X, css, cur.t0, lane, lds);
+            if (css + 1 == cur.S) {
+                finish_seg(cur, acc, lane, lds, tables, out);
+                acc = 0;
+            }
+            cur = nx;
+            css = nss;
+            return have;
+        };
+        while (step(bufA, bufB) && step(bufB, bufA)) {
+        }
+        return;
     }
 
     const uint32_t *ztab = tables + ZDBCRC_OFF_Z;
@@ -332,9 +439,10 @@ struct KernelVariant {
 
 // selectable with ZDBCRC_VARIANT=<index> (A/B measurement); 0 is the default
 const KernelVariant kVariants[] = {
-    {"wg512_w4", crc_batch_kernel<512, 4>, 512},
-    {"wg768_w6", crc_batch_kernel<768, 6>, 768},
-    {"wg1024_w4", crc_batch_kernel<1024, 4>, 1024},
+    {"wg512_w4_pipe", crc_batch_kernel<512, 4, true>, 512},
+    {"wg512_w4", crc_batch_kernel<512, 4, false>, 512},
+    {"wg768_w6_pipe", crc_batch_kernel<768, 6, true>, 768},
+    {"wg768_w6", crc_batch_kernel<768, 6, false>, 768},
 };
 
 constexpr int kNumVariants = (int)(sizeof(kVariants) / sizeof(kVariants[0]));
