@@ -174,13 +174,31 @@ __device__ __forceinline__ void load_superstep(const SegCtx &s, uint32_t ss, uin
         buf[i] = load_piece<CHECK>(s, ss * K + i, lane);
 }
 
-// zero the bytes of a piece that lie outside the record (first/last piece only)
+// zero the bytes of a piece that lie outside the record (first/last piece
+// only) and whole pieces before the segment (lanes whose load was clamped)
 __device__ __forceinline__ uint4 fix_edges(const SegCtx &s, uint4 v, uint32_t t, uint32_t lane) {
     const int64_t jj = s.base_j + 64 * (int64_t)t + (int64_t)lane;
     const bool first = jj == 0, last = jj == (int64_t)s.np - 1;
     if (first || last)
         v = mask_piece(v, first ? s.lo0 : 0, last ? s.hi_last : 16);
+    if (jj < (int64_t)s.pa)
+        v = make_uint4(0, 0, 0, 0);
     return v;
+}
+
+// unconditional loads of one superstep: lanes before the segment read the
+// segment's first piece instead (zeroed later by fix_edges), so the VMEM
+// instruction stream is the same on every path and the compiler's counted
+// waits stay exact
+__device__ __forceinline__ void load_superstep_clamped(const SegCtx &s, uint32_t ss, uint32_t lane,
+                                                       uint4 (&buf)[K]) {
+#pragma unroll
+    for (int i = 0; i < K; i++) {
+        int64_t jj = s.base_j + 64 * (int64_t)(ss * K + i) + (int64_t)lane;
+        jj = jj < (int64_t)s.pa ? (int64_t)s.pa : jj;
+        const u32x4 v = *reinterpret_cast<global_u32x4 *>(s.P0 + 16u * (uint64_t)jj);
+        buf[i] = make_uint4(v.x, v.y, v.z, v.w);
+    }
 }
 
 // one superstep (K steps) folded into the lane register.  Only the first
@@ -283,6 +301,19 @@ __device__ __forceinline__ bool next_seg(uint64_t &r, uint64_t n, uint64_t ub, u
     }
 }
 
+// lane registers -> the segment's contribution to crc(record)
+__device__ __forceinline__ uint32_t seg_value(const Seg &sg, uint32_t acc, uint32_t lane, const uint32_t *lds,
+                                              const uint32_t *__restrict__ tables) {
+    uint32_t x = __builtin_amdgcn_readfirstlane(wave_xor(lane_place(acc, lane, lds)));
+    if (sg.z) // remove the zero bytes that pad the record's last piece
+        x = uniform_shift(x, tables + ZDBCRC_OFF_Z + sg.z * SCH * 32);
+    uint64_t q = sg.c.np - sg.pb; // record pieces after this segment
+    for (int g = 0; q; g++, q >>= 1)
+        if (q & 1)
+            x = uniform_shift(x, tables + ZDBCRC_OFF_G + g * SCH * 32);
+    return x;
+}
+
 // lane registers -> record contribution -> out[r]
 __device__ __forceinline__ void finish_seg(const Seg &sg, uint32_t acc, uint32_t lane, const uint32_t *lds,
                                            const uint32_t *__restrict__ tables, uint32_t *__restrict__ out) {
@@ -307,7 +338,8 @@ template <int WGT, int WPE, bool PIPE>
 __global__ __launch_bounds__(WGT, WPE) void crc_batch_kernel(
     const uint8_t *__restrict__ arena, const uint64_t *__restrict__ offsets,
     const uint32_t *__restrict__ lengths, const uint64_t *__restrict__ unit_start, uint64_t n,
-    uint32_t *__restrict__ out, const uint32_t *__restrict__ tables, uint32_t max_waves) {
+    uint32_t *__restrict__ out, const uint32_t *__restrict__ tables, uint32_t max_waves,
+    uint32_t *__restrict__ scratch) {
     __shared__ __attribute__((aligned(16))) uint32_t lds[ZDBCRC_LDS_DW];
 
     {
@@ -342,41 +374,66 @@ __global__ __launch_bounds__(WGT, WPE) void crc_batch_kernel(
     }
 
     if (PIPE) {
-        // one stream of supersteps over all of the slice's segments; the next
-        // superstep's loads (possibly of the next record) are in flight while
-        // the current one is folded
+        // One stream of supersteps over the slice's segments.  Every
+        // iteration issues the same VMEM sequence -- 4 clamped loads for the
+        // NEXT superstep (of this segment or the next one), then one store --
+        // so the waits the compiler counts are exact and the next loads stay
+        // in flight while the current superstep is folded.  Whole segments
+        // store out[r]; iterations that finish nothing store to the wave's
+        // scratch slot; the (at most two) segments cut by the slice edges are
+        // XORed into out[] after the loop.
         uint64_t rn = lo;
         Seg cur, nx;
         if (!next_seg(rn, n, ub, ue, unit_start, arena, offsets, lengths, cur))
             return;
+        uint32_t *const dummy = scratch + gw;
+        uint64_t cut_r[2] = {0, 0};
+        uint32_t cut_x[2] = {0, 0}, ncut = 0;
         uint32_t css = 0, acc = 0;
-        uint4 bufA[K], bufB[K];
-        load_superstep<true>(cur.c, 0, lane, bufA);
-        auto step = [&](const uint4(&X)[K], uint4(&Y)[K]) -> bool {
+        uint4 bufc[K], bufn[K];
+        load_superstep_clamped(cur.c, 0, lane, bufc);
+        for (;;) {
             uint32_t nss = 0;
-            bool have = true;
+            bool more = true;
             if (css + 1 < cur.S) {
                 nx = cur;
                 nss = css + 1;
-                load_superstep<false>(nx.c, nss, lane, Y);
-            } else {
-                have = next_seg(rn, n, ub, ue, unit_start, arena, offsets, lengths, nx);
-                if (have)
-                    load_superstep<true>(nx.c, 0, lane, Y);
+            } else if (!next_seg(rn, n, ub, ue, unit_start, arena, offsets, lengths, nx)) {
+                more = false;
+                nx = cur; // harmless re-load keeps the VMEM stream uniform
+                nss = css;
             }
+            load_superstep_clamped(nx.c, nss, lane, bufn);
             if (css == 0 || css + 1 == cur.S)
-                acc = superstep<true>(cur.c, acc, X, css, cur.t0, lane, lds);
+                acc = superstep<true>(cur.c, acc, bufc, css, cur.t0, lane, lds);
             else
-                acc = superstep<false>(cur.c, acc, X, css, cur.t0, lane, lds);
+                acc = superstep<false>(cur.c, acc, bufc, css, cur.t0, lane, lds);
+            uint32_t *dst = dummy;
+            uint32_t x = 0;
             if (css + 1 == cur.S) {
-                finish_seg(cur, acc, lane, lds, tables, out);
+                x = seg_value(cur, acc, lane, lds, tables);
                 acc = 0;
+                if (cur.c.pa == 0 && cur.pb == cur.c.np) {
+                    dst = out + cur.r;
+                } else {
+                    cut_r[ncut & 1] = cur.r;
+                    cut_x[ncut & 1] = x;
+                    ncut++;
+                }
             }
+            if (lane == 0)
+                *dst = x;
+            if (!more)
+                break;
             cur = nx;
             css = nss;
-            return have;
-        };
-        while (step(bufA, bufB) && step(bufB, bufA)) {
+#pragma unroll
+            for (int i = 0; i < K; i++)
+                bufc[i] = bufn[i];
+        }
+        if (lane == 0) {
+            for (uint32_t i = 0; i < ncut && i < 2; i++)
+                atomicXor(out + cut_r[i], cut_x[i]);
         }
         return;
     }
@@ -429,7 +486,7 @@ __global__ __launch_bounds__(WGT, WPE) void crc_batch_kernel(
 }
 
 typedef void (*crc_kernel_fn)(const uint8_t *, const uint64_t *, const uint32_t *, const uint64_t *, uint64_t,
-                              uint32_t *, const uint32_t *, uint32_t);
+                              uint32_t *, const uint32_t *, uint32_t, uint32_t *);
 
 struct KernelVariant {
     const char *name;
@@ -442,7 +499,7 @@ const KernelVariant kVariants[] = {
     {"wg512_w4_pipe", crc_batch_kernel<512, 4, true>, 512},
     {"wg512_w4", crc_batch_kernel<512, 4, false>, 512},
     {"wg768_w6_pipe", crc_batch_kernel<768, 6, true>, 768},
-    {"wg768_w6", crc_batch_kernel<768, 6, false>, 768},
+    {"wg1024_w8_pipe", crc_batch_kernel<1024, 8, true>, 1024},
 };
 
 constexpr int kNumVariants = (int)(sizeof(kVariants) / sizeof(kVariants[0]));
@@ -586,7 +643,8 @@ int enqueue_batch(DeviceCtx &c, const uint8_t *arena, const uint64_t *offsets, c
 
     const size_t us_bytes = ((n + 1) * sizeof(uint64_t) + 255) & ~size_t(255);
     const size_t tmp_bytes = scan_temp_bytes(n);
-    const size_t need = us_bytes + tmp_bytes + 256;
+    const size_t scratch_bytes = 64 * 1024; // one dword per wave of the grid
+    const size_t need = us_bytes + scratch_bytes + tmp_bytes + 256;
     Workspace &w = c.ws[reinterpret_cast<void *>(st)];
     if (w.bytes < need) {
         if (w.ptr) {
@@ -600,7 +658,8 @@ int enqueue_batch(DeviceCtx &c, const uint8_t *arena, const uint64_t *offsets, c
         w.bytes = need;
     }
     uint64_t *unit_start = static_cast<uint64_t *>(w.ptr);
-    void *tmp = static_cast<uint8_t *>(w.ptr) + us_bytes;
+    uint32_t *scratch = reinterpret_cast<uint32_t *>(static_cast<uint8_t *>(w.ptr) + us_bytes);
+    void *tmp = static_cast<uint8_t *>(w.ptr) + us_bytes + scratch_bytes;
     size_t tb = tmp_bytes;
     auto it = rocprim::make_transform_iterator(rocprim::counting_iterator<uint64_t>(0),
                                                UnitCount{arena, offsets, lengths, n});
@@ -624,7 +683,7 @@ int enqueue_batch(DeviceCtx &c, const uint8_t *arena, const uint64_t *offsets, c
         hipEventRecord(e0, st);
     }
     hipLaunchKernelGGL(kv.fn, dim3(grid), dim3(kv.threads), 0, st, arena, offsets, lengths, unit_start, n,
-                       out, c.d_tables, max_waves);
+                       out, c.d_tables, max_waves, scratch);
     if (hipGetLastError() != hipSuccess)
         return ZDB_CRC32_ELAUNCH;
     if (g_timing) {
