@@ -69,6 +69,10 @@ __device__ __forceinline__ uint32_t word_of(const uint4 &v, int d) {
     return d == 0 ? v.x : d == 1 ? v.y : d == 2 ? v.z : v.w;
 }
 
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96); // a ^ b ^ c in one VALU op
+}
+
 // 5-bit slice c (bits [5c, 5c+5)) of a little-endian 128-bit piece.
 // c is a compile-time constant after unrolling.
 __device__ __forceinline__ uint32_t piece_slice(const uint4 &v, int c) {
@@ -80,17 +84,25 @@ __device__ __forceinline__ uint32_t piece_slice(const uint4 &v, int c) {
 
 // contribution of one piece in slot I of a superstep: 26 conflict-free
 // lookups, folded three at a time (v_bitop3 xor3) in issue order
-template <int I>
+// MODE is a measurement ablation: 0 = real lookups; 1 = same slicing, no
+// LDS (XOR of the addresses); 2 = data only.  Only MODE 0 is a checksum.
+template <int I, int MODE = 0>
 __device__ __forceinline__ uint32_t piece_contrib(const uint4 &v, const uint32_t *lds) {
-    const uint32_t *tab = lds + ZDBCRC_OFF_T + I * PCH * 32;
-    uint32_t r = tab[(PCH - 2) * 32 + piece_slice(v, PCH - 2)] ^ tab[(PCH - 1) * 32 + piece_slice(v, PCH - 1)];
+    if (MODE == 2)
+        return v.x ^ v.y ^ v.z ^ v.w;
+    if (MODE == 1) {
+        uint32_t r = 0;
 #pragma unroll
-    for (int c = 0; c + 2 < PCH; c += 3) {
-        const uint32_t a = tab[c * 32 + piece_slice(v, c)];
-        const uint32_t b = tab[(c + 1) * 32 + piece_slice(v, c + 1)];
-        const uint32_t d = tab[(c + 2) * 32 + piece_slice(v, c + 2)];
-        r = r ^ a ^ b ^ d;
+        for (int c = 0; c < PCH; c++)
+            r ^= (ZDBCRC_OFF_T + (I * PCH + c) * 32 + piece_slice(v, c)) * 4u;
+        return r;
     }
+    const uint32_t *tab = lds + ZDBCRC_OFF_T + I * PCH * 32;
+    // 26 lookups folded two per v_bitop3 (three-input XOR)
+    uint32_t r = 0;
+#pragma unroll
+    for (int c = 0; c < PCH; c += 2)
+        r = xor3(r, tab[c * 32 + piece_slice(v, c)], tab[(c + 1) * 32 + piece_slice(v, c + 1)]);
     return r;
 }
 
@@ -205,7 +217,7 @@ __device__ __forceinline__ void load_superstep_clamped(const SegCtx &s, uint32_t
 // superstep can hold empty leading steps / lanes and the record's first
 // piece; only the last can hold the record's last piece: EDGE enables the
 // checks there, the middle supersteps run without them.
-template <bool EDGE>
+template <bool EDGE, int MODE = 0>
 __device__ __forceinline__ uint32_t superstep(const SegCtx &s, uint32_t acc, const uint4 (&cur)[K], uint32_t ss,
                                               uint32_t t0, uint32_t lane, const uint32_t *lds) {
     if (ss)
@@ -213,7 +225,7 @@ __device__ __forceinline__ uint32_t superstep(const SegCtx &s, uint32_t acc, con
     const uint32_t tb = ss * K;
 #define ZDBCRC_SLOT(I)                                                                   \
     if (tb + I >= t0)                                                                    \
-        acc ^= piece_contrib<I>(EDGE ? fix_edges(s, cur[I], tb + I, lane) : cur[I], lds);
+        acc ^= piece_contrib<I, MODE>(EDGE ? fix_edges(s, cur[I], tb + I, lane) : cur[I], lds);
 
     ZDBCRC_SLOT(0)
     ZDBCRC_SLOT(1)
@@ -334,7 +346,7 @@ __device__ __forceinline__ void finish_seg(const Seg &sg, uint32_t acc, uint32_t
 
 // WGT threads per workgroup, WPE = minimum waves per SIMD (register budget),
 // PIPE: loads run one superstep ahead across record boundaries too
-template <int WGT, int WPE, bool PIPE>
+template <int WGT, int WPE, bool PIPE, int MODE = 0>
 __global__ __launch_bounds__(WGT, WPE) void crc_batch_kernel(
     const uint8_t *__restrict__ arena, const uint64_t *__restrict__ offsets,
     const uint32_t *__restrict__ lengths, const uint64_t *__restrict__ unit_start, uint64_t n,
@@ -405,9 +417,9 @@ __global__ __launch_bounds__(WGT, WPE) void crc_batch_kernel(
             }
             load_superstep_clamped(nx.c, nss, lane, bufn);
             if (css == 0 || css + 1 == cur.S)
-                acc = superstep<true>(cur.c, acc, bufc, css, cur.t0, lane, lds);
+                acc = superstep<true, MODE>(cur.c, acc, bufc, css, cur.t0, lane, lds);
             else
-                acc = superstep<false>(cur.c, acc, bufc, css, cur.t0, lane, lds);
+                acc = superstep<false, MODE>(cur.c, acc, bufc, css, cur.t0, lane, lds);
             uint32_t *dst = dummy;
             uint32_t x = 0;
             if (css + 1 == cur.S) {
@@ -485,6 +497,212 @@ __global__ __launch_bounds__(WGT, WPE) void crc_batch_kernel(
     }
 }
 
+// ---------------------------------------------------------------------------
+// v3: pipelined stream + lane-parallel record metadata + DPP reduction
+// ---------------------------------------------------------------------------
+
+__device__ __forceinline__ uint64_t readlane64(uint64_t v, uint32_t l) {
+    const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)v, l);
+    const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(v >> 32), l);
+    return ((uint64_t)hi << 32) | lo;
+}
+
+// XOR of a value over the 64 lanes, as a wave-uniform scalar: DPP within
+// rows of 16 (VALU, no LDS traffic), then four readlanes
+__device__ __forceinline__ uint32_t wave_xor_scalar(uint32_t x) {
+    x ^= __builtin_amdgcn_update_dpp(0u, x, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
+    x ^= __builtin_amdgcn_update_dpp(0u, x, 0x4E, 0xF, 0xF, false);  // quad_perm [2,3,0,1]
+    x ^= __builtin_amdgcn_update_dpp(0u, x, 0x124, 0xF, 0xF, false); // row_ror:4
+    x ^= __builtin_amdgcn_update_dpp(0u, x, 0x128, 0xF, 0xF, false); // row_ror:8
+    return __builtin_amdgcn_readlane(x, 0) ^ __builtin_amdgcn_readlane(x, 16) ^
+           __builtin_amdgcn_readlane(x, 32) ^ __builtin_amdgcn_readlane(x, 48);
+}
+
+// metadata of 64 consecutive records [rb, rb+64), record rb+l on lane l
+struct MetaBatch {
+    uint64_t rb;   // uniform
+    uint64_t u0;   // unit_start[r]
+    uint64_t ur;   // unit_start[r+1]
+    uint64_t addr; // arena address of the record
+    uint32_t len;
+};
+
+__device__ __forceinline__ void load_meta(MetaBatch &m, uint64_t rb, uint64_t n, uint32_t lane,
+                                          const uint64_t *__restrict__ unit_start, const uint8_t *arena,
+                                          const uint64_t *__restrict__ offsets,
+                                          const uint32_t *__restrict__ lengths) {
+    m.rb = rb;
+    const uint64_t r = rb + lane;
+    m.u0 = ~0ull;
+    m.ur = ~0ull;
+    m.addr = 0;
+    m.len = 0;
+    if (r < n) {
+        m.u0 = unit_start[r];
+        m.ur = unit_start[r + 1];
+        m.addr = reinterpret_cast<uint64_t>(arena) + offsets[r];
+        m.len = lengths[r];
+    }
+}
+
+__device__ __forceinline__ bool next_seg_batched(uint64_t &r, uint64_t n, uint64_t ub, uint64_t ue, uint32_t lane,
+                                                 MetaBatch &m, const uint64_t *__restrict__ unit_start,
+                                                 const uint8_t *arena, const uint64_t *__restrict__ offsets,
+                                                 const uint32_t *__restrict__ lengths, Seg &sg) {
+    for (;;) {
+        if (r >= n)
+            return false;
+        if (r >= m.rb + 64)
+            load_meta(m, r, n, lane, unit_start, arena, offsets, lengths);
+        const uint32_t li = (uint32_t)(r - m.rb);
+        const uint64_t u0 = readlane64(m.u0, li);
+        if (u0 >= ue)
+            return false;
+        const uint64_t us = u0 + UNIT_OVH;
+        const uint64_t ur = readlane64(m.ur, li);
+        const uint64_t s_lo = ub > us ? ub : us;
+        const uint64_t s_hi = ue < ur ? ue : ur;
+        if (s_hi > s_lo) {
+            const uint64_t A = readlane64(m.addr, li);
+            const uint64_t Aend = A + __builtin_amdgcn_readlane(m.len, li);
+            sg.r = r;
+            sg.c.P0 = A & ~15ull;
+            sg.c.np = (uint32_t)(ur - us);
+            sg.z = (uint32_t)(sg.c.P0 + 16u * (uint64_t)sg.c.np - Aend);
+            sg.c.lo0 = (int)(A & 15u);
+            sg.c.hi_last = 16 - (int)sg.z;
+            sg.c.pa = (uint32_t)(s_lo - us);
+            sg.pb = (uint32_t)(s_hi - us);
+            const uint32_t T = (sg.pb - sg.c.pa + 63u) / 64u;
+            sg.S = (T + K - 1) / K;
+            sg.t0 = sg.S * K - T;
+            sg.c.base_j = (int64_t)sg.pb - 64 * (int64_t)sg.S * K;
+            r++;
+            return true;
+        }
+        r++;
+    }
+}
+
+// loads of superstep ss: uniform base (segment's first piece) + 32-bit lane
+// offset; lanes before the segment re-read its first piece (zeroed later)
+__device__ __forceinline__ void load_superstep_v3(const SegCtx &s, uint32_t ss, uint32_t lane, uint4 (&buf)[K]) {
+    const uint64_t base = s.P0 + 16u * (uint64_t)s.pa;
+    const int32_t rel0 = (int32_t)(s.base_j - (int64_t)s.pa) + 64 * (int32_t)(ss * K) + (int32_t)lane;
+#pragma unroll
+    for (int i = 0; i < K; i++) {
+        int32_t rel = rel0 + 64 * i;
+        rel = rel < 0 ? 0 : rel;
+        const u32x4 v = *reinterpret_cast<global_u32x4 *>(base + ((uint64_t)(uint32_t)rel << 4));
+        buf[i] = make_uint4(v.x, v.y, v.z, v.w);
+    }
+}
+
+__device__ __forceinline__ uint32_t seg_value_v3(const Seg &sg, uint32_t acc, uint32_t lane, const uint32_t *lds,
+                                                 const uint32_t *__restrict__ tables) {
+    uint32_t x = wave_xor_scalar(lane_place(acc, lane, lds));
+    if (sg.z)
+        x = uniform_shift(x, tables + ZDBCRC_OFF_Z + sg.z * SCH * 32);
+    uint64_t q = sg.c.np - sg.pb;
+    for (int g = 0; q; g++, q >>= 1)
+        if (q & 1)
+            x = uniform_shift(x, tables + ZDBCRC_OFF_G + g * SCH * 32);
+    return x;
+}
+
+template <int WGT, int WPE>
+__global__ __launch_bounds__(WGT, WPE) void crc_batch_kernel_v3(
+    const uint8_t *__restrict__ arena, const uint64_t *__restrict__ offsets,
+    const uint32_t *__restrict__ lengths, const uint64_t *__restrict__ unit_start, uint64_t n,
+    uint32_t *__restrict__ out, const uint32_t *__restrict__ tables, uint32_t max_waves,
+    uint32_t *__restrict__ scratch) {
+    __shared__ __attribute__((aligned(16))) uint32_t lds[ZDBCRC_LDS_DW];
+    {
+        const uint4 *src = reinterpret_cast<const uint4 *>(tables);
+        uint4 *dst = reinterpret_cast<uint4 *>(lds);
+        for (int i = threadIdx.x; i < ZDBCRC_LDS_DW / 4; i += WGT)
+            dst[i] = src[i];
+    }
+    __syncthreads();
+
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t gw = __builtin_amdgcn_readfirstlane(blockIdx.x * (WGT / 64) + (threadIdx.x >> 6));
+    const uint64_t total = unit_start[n];
+    uint64_t nwaves = (total + MIN_UNITS_PER_WAVE - 1) / MIN_UNITS_PER_WAVE;
+    if (nwaves > max_waves)
+        nwaves = max_waves;
+    if (gw >= nwaves)
+        return;
+    const uint64_t ub = total * gw / nwaves;
+    const uint64_t ue = total * (gw + 1) / nwaves;
+    if (ub >= ue)
+        return;
+    uint64_t lo = 0, hi = n;
+    while (hi - lo > 1) {
+        const uint64_t mid = (lo + hi) >> 1;
+        if (unit_start[mid] <= ub)
+            lo = mid;
+        else
+            hi = mid;
+    }
+
+    MetaBatch m;
+    load_meta(m, lo, n, lane, unit_start, arena, offsets, lengths);
+    uint64_t rn = lo;
+    Seg cur, nx;
+    if (!next_seg_batched(rn, n, ub, ue, lane, m, unit_start, arena, offsets, lengths, cur))
+        return;
+    uint32_t *const dummy = scratch + gw;
+    uint64_t cut_r[2] = {0, 0};
+    uint32_t cut_x[2] = {0, 0}, ncut = 0;
+    uint32_t css = 0, acc = 0;
+    uint4 bufc[K], bufn[K];
+    load_superstep_v3(cur.c, 0, lane, bufc);
+    for (;;) {
+        uint32_t nss = 0;
+        bool more = true;
+        if (css + 1 < cur.S) {
+            nx = cur;
+            nss = css + 1;
+        } else if (!next_seg_batched(rn, n, ub, ue, lane, m, unit_start, arena, offsets, lengths, nx)) {
+            more = false;
+            nx = cur;
+            nss = css;
+        }
+        load_superstep_v3(nx.c, nss, lane, bufn);
+        if (css == 0 || css + 1 == cur.S)
+            acc = superstep<true>(cur.c, acc, bufc, css, cur.t0, lane, lds);
+        else
+            acc = superstep<false>(cur.c, acc, bufc, css, cur.t0, lane, lds);
+        uint32_t *dst = dummy;
+        uint32_t x = 0;
+        if (css + 1 == cur.S) {
+            x = seg_value_v3(cur, acc, lane, lds, tables);
+            acc = 0;
+            if (cur.c.pa == 0 && cur.pb == cur.c.np) {
+                dst = out + cur.r;
+            } else {
+                cut_r[ncut & 1] = cur.r;
+                cut_x[ncut & 1] = x;
+                ncut++;
+            }
+        }
+        if (lane == 0)
+            *dst = x;
+        if (!more)
+            break;
+        cur = nx;
+        css = nss;
+#pragma unroll
+        for (int i = 0; i < K; i++)
+            bufc[i] = bufn[i];
+    }
+    if (lane == 0) {
+        for (uint32_t i = 0; i < ncut && i < 2; i++)
+            atomicXor(out + cut_r[i], cut_x[i]);
+    }
+}
+
 typedef void (*crc_kernel_fn)(const uint8_t *, const uint64_t *, const uint32_t *, const uint64_t *, uint64_t,
                               uint32_t *, const uint32_t *, uint32_t, uint32_t *);
 
@@ -496,10 +714,15 @@ struct KernelVariant {
 
 // selectable with ZDBCRC_VARIANT=<index> (A/B measurement); 0 is the default
 const KernelVariant kVariants[] = {
+    {"v3_wg768", crc_batch_kernel_v3<768, 6>, 768},
+    {"v3_wg1024", crc_batch_kernel_v3<1024, 8>, 1024},
+    {"v3_wg512", crc_batch_kernel_v3<512, 4>, 512},
     {"wg512_w4_pipe", crc_batch_kernel<512, 4, true>, 512},
     {"wg512_w4", crc_batch_kernel<512, 4, false>, 512},
     {"wg768_w6_pipe", crc_batch_kernel<768, 6, true>, 768},
     {"wg1024_w8_pipe", crc_batch_kernel<1024, 8, true>, 1024},
+    {"ablate_nolds", crc_batch_kernel<1024, 8, true, 1>, 1024},
+    {"ablate_loadonly", crc_batch_kernel<1024, 8, true, 2>, 1024},
 };
 
 constexpr int kNumVariants = (int)(sizeof(kVariants) / sizeof(kVariants[0]));
@@ -540,6 +763,62 @@ __global__ void verify_kernel(const uint32_t *__restrict__ out, const uint32_t *
         if (idx < max_mismatch)
             mismatch[idx] = (uint32_t)r;
     }
+}
+
+// read-only streaming probe (measurement aid): XOR of every 16-byte word,
+// one dword written per workgroup -- the achievable HBM read ceiling the
+// checksum kernel is compared with
+__global__ __launch_bounds__(256) void stream_read_kernel(const uint4 *__restrict__ src, uint64_t words,
+                                                          uint32_t *__restrict__ sink) {
+    uint4 a = make_uint4(0, 0, 0, 0), b = a, c = a, d = a;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    for (; i + 3 * stride < words; i += 4 * stride) {
+        const uint4 x0 = src[i], x1 = src[i + stride], x2 = src[i + 2 * stride], x3 = src[i + 3 * stride];
+        a.x ^= x0.x; a.y ^= x0.y; a.z ^= x0.z; a.w ^= x0.w;
+        b.x ^= x1.x; b.y ^= x1.y; b.z ^= x1.z; b.w ^= x1.w;
+        c.x ^= x2.x; c.y ^= x2.y; c.z ^= x2.z; c.w ^= x2.w;
+        d.x ^= x3.x; d.y ^= x3.y; d.z ^= x3.z; d.w ^= x3.w;
+    }
+    for (; i < words; i += stride) {
+        const uint4 x0 = src[i];
+        a.x ^= x0.x; a.y ^= x0.y; a.z ^= x0.z; a.w ^= x0.w;
+    }
+    uint32_t v = a.x ^ a.y ^ a.z ^ a.w ^ b.x ^ b.y ^ b.z ^ b.w ^ c.x ^ c.y ^ c.z ^ c.w ^ d.x ^ d.y ^ d.z ^ d.w;
+    v = wave_xor(v);
+    if ((threadIdx.x & 63) == 0)
+        atomicXor(sink + blockIdx.x, v);
+}
+
+// contiguous-slice variant of the probe: wave w reads its own slice, 1 KiB
+// per load instruction, U loads per lane per iteration -- the access shape of
+// crc_batch_kernel without any checksum work
+template <int U>
+__global__ __launch_bounds__(1024) void stream_slice_kernel(const uint4 *__restrict__ src, uint64_t words,
+                                                            uint32_t *__restrict__ sink) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t nw = (uint64_t)gridDim.x * (blockDim.x / 64);
+    const uint64_t w = (uint64_t)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
+    const uint64_t lo = words * w / nw, hi = words * (w + 1) / nw;
+    uint4 a = make_uint4(0, 0, 0, 0);
+    uint64_t i = lo + lane;
+    for (; i + 64 * (U - 1) < hi; i += 64 * U) {
+        uint4 x[U];
+#pragma unroll
+        for (int u = 0; u < U; u++)
+            x[u] = src[i + 64 * u];
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            a.x ^= x[u].x; a.y ^= x[u].y; a.z ^= x[u].z; a.w ^= x[u].w;
+        }
+    }
+    for (; i < hi; i += 64) {
+        const uint4 x0 = src[i];
+        a.x ^= x0.x; a.y ^= x0.y; a.z ^= x0.z; a.w ^= x0.w;
+    }
+    uint32_t v = wave_xor(a.x ^ a.y ^ a.z ^ a.w);
+    if (lane == 0)
+        atomicXor(sink + (w & 0xFFFF), v);
 }
 
 __device__ __forceinline__ uint64_t mix64(uint64_t z) {
@@ -728,6 +1007,35 @@ const char *zdb_crc32_batch_engine(void) {
 }
 
 int zdb_crc32_gpu_initialized(void) { return g_hip_touched ? 1 : 0; }
+
+// measurement hook (not part of the public ABI): time a read-only stream of
+// `bytes` (multiple of 16) with HIP events; returns ms, <0 on error
+float zdbcrc_debug_stream_read(const void *d_buf, size_t bytes, uint32_t *d_sink, int blocks, void *stream) {
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    hipEvent_t a, b;
+    hipEventCreate(&a);
+    hipEventCreate(&b);
+    hipEventRecord(a, st);
+    const uint4 *src = static_cast<const uint4 *>(d_buf);
+    const uint64_t words = bytes / 16;
+    // blocks > 0: grid-stride probe with that many 256-thread blocks;
+    // blocks = -U: contiguous-slice probe, 512 x 1024-thread blocks, U loads/lane
+    if (blocks > 0)
+        hipLaunchKernelGGL(stream_read_kernel, dim3(blocks), dim3(256), 0, st, src, words, d_sink);
+    else if (blocks == -4)
+        hipLaunchKernelGGL(stream_slice_kernel<4>, dim3(512), dim3(1024), 0, st, src, words, d_sink);
+    else if (blocks == -8)
+        hipLaunchKernelGGL(stream_slice_kernel<8>, dim3(512), dim3(1024), 0, st, src, words, d_sink);
+    else
+        hipLaunchKernelGGL(stream_slice_kernel<16>, dim3(512), dim3(1024), 0, st, src, words, d_sink);
+    hipEventRecord(b, st);
+    float ms = -1;
+    if (hipEventSynchronize(b) == hipSuccess)
+        hipEventElapsedTime(&ms, a, b);
+    hipEventDestroy(a);
+    hipEventDestroy(b);
+    return ms;
+}
 
 // measurement hook (not part of the public ABI): select a kernel variant for
 // A/B timing in one process; returns its name, NULL if out of range

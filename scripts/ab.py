@@ -20,6 +20,17 @@ while True:
     if not n:
         break
     names.append(n.decode()); i += 1
+probe = zdbcrc._lib.zdbcrc_debug_stream_read
+probe.restype = C.c_float
+probe.argtypes = [C.c_void_p, C.c_size_t, C.c_void_p, C.c_int, C.c_void_p]
+buf = torch.empty(4 << 30, dtype=torch.uint8, device="cuda"); buf.fill_(7)
+sink = torch.zeros(1 << 16, dtype=torch.int32, device="cuda")
+st = torch.cuda.current_stream().cuda_stream
+for blocks in (2048, 8192, 16384, -4, -8, -16):
+    ts = [probe(buf.data_ptr(), buf.numel(), sink.data_ptr(), blocks, st) for _ in range(6)][1:]
+    print(json.dumps({"probe": "stream_read_4GiB", "blocks": blocks, "median_ms": round(float(np.median(ts)), 4),
+                      "tbs": round(buf.numel() / (np.median(ts) / 1e3) / 1e12, 3)}), flush=True)
+del buf
 sel = [int(x) for x in sys.argv[2].split(",")] if len(sys.argv) > 2 else list(range(len(names)))
 work = sys.argv[1] if len(sys.argv) > 1 else "zipf"
 ROUNDS, STEPS = 5, 5
@@ -27,6 +38,10 @@ for wl in work.split(","):
     if wl == "zipf":
         lens = zdbcrc.zipf_lengths(4 << 30, 0xC3C3C3).astype(np.int64)
         seed = 0x5A0DB5EED + 3
+    elif wl == "single":
+        lens = np.array([(4 << 30) - 16], np.int64); seed = 0x5A0DB5EED
+    elif wl == "fixed64k":
+        lens = np.full(1 << 16, 65536, np.int64); seed = 0x5A0DB5EED
     else:
         lens = np.full(1 << 20, 4096, np.int64); seed = 0x5A0DB5EED
     offs = np.zeros(len(lens), np.int64); offs[1:] = np.cumsum(lens[:-1])
