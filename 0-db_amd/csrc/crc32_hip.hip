@@ -213,6 +213,16 @@ __device__ __forceinline__ void load_superstep_clamped(const SegCtx &s, uint32_t
     }
 }
 
+// fix_edges only where the step (64 pieces, wave-uniform range) holds a
+// partial first/last piece or lanes before the segment
+__device__ __forceinline__ uint4 edge_piece(const SegCtx &s, uint4 v, uint32_t t, uint32_t lane) {
+    const int64_t j0 = s.base_j + 64 * (int64_t)t;
+    const int64_t jl = (int64_t)s.np - 1;
+    const bool need = j0 < (int64_t)s.pa || (s.lo0 != 0 && j0 <= 0 && 0 <= j0 + 63) ||
+                      (s.hi_last != 16 && j0 <= jl && jl <= j0 + 63);
+    return need ? fix_edges(s, v, t, lane) : v;
+}
+
 // one superstep (K steps) folded into the lane register.  Only the first
 // superstep can hold empty leading steps / lanes and the record's first
 // piece; only the last can hold the record's last piece: EDGE enables the
@@ -224,8 +234,8 @@ __device__ __forceinline__ uint32_t superstep(const SegCtx &s, uint32_t acc, con
         acc = advance_superstep(acc, lds);
     const uint32_t tb = ss * K;
 #define ZDBCRC_SLOT(I)                                                                   \
-    if (tb + I >= t0)                                                                    \
-        acc ^= piece_contrib<I, MODE>(EDGE ? fix_edges(s, cur[I], tb + I, lane) : cur[I], lds);
+    if (!EDGE || tb + I >= t0)                                                           \
+        acc ^= piece_contrib<I, MODE>(EDGE ? edge_piece(s, cur[I], tb + I, lane) : cur[I], lds);
 
     ZDBCRC_SLOT(0)
     ZDBCRC_SLOT(1)
