@@ -925,13 +925,15 @@ size_t scan_temp_bytes(uint64_t n) {
 }
 
 // enqueue memset + plan scan + main kernel; caller holds g_mu
+// d_unit_start: the per-record unit prefix when the caller already has it
+// (host-planned batches); nullptr -> computed on the device by the scan
 int enqueue_batch(DeviceCtx &c, const uint8_t *arena, const uint64_t *offsets, const uint32_t *lengths,
-                  uint32_t *out, uint64_t n, hipStream_t st) {
+                  uint32_t *out, uint64_t n, hipStream_t st, const uint64_t *d_unit_start = nullptr) {
     if (hipMemsetAsync(out, 0, n * sizeof(uint32_t), st) != hipSuccess)
         return ZDB_CRC32_ELAUNCH;
 
-    const size_t us_bytes = ((n + 1) * sizeof(uint64_t) + 255) & ~size_t(255);
-    const size_t tmp_bytes = scan_temp_bytes(n);
+    const size_t us_bytes = d_unit_start ? 0 : ((n + 1) * sizeof(uint64_t) + 255) & ~size_t(255);
+    const size_t tmp_bytes = d_unit_start ? 0 : scan_temp_bytes(n);
     const size_t scratch_bytes = 64 * 1024; // one dword per wave of the grid
     const size_t need = us_bytes + scratch_bytes + tmp_bytes + 256;
     Workspace &w = c.ws[reinterpret_cast<void *>(st)];
@@ -946,15 +948,19 @@ int enqueue_batch(DeviceCtx &c, const uint8_t *arena, const uint64_t *offsets, c
             return ZDB_CRC32_ENOMEM;
         w.bytes = need;
     }
-    uint64_t *unit_start = static_cast<uint64_t *>(w.ptr);
+    const uint64_t *unit_start = d_unit_start;
     uint32_t *scratch = reinterpret_cast<uint32_t *>(static_cast<uint8_t *>(w.ptr) + us_bytes);
-    void *tmp = static_cast<uint8_t *>(w.ptr) + us_bytes + scratch_bytes;
-    size_t tb = tmp_bytes;
-    auto it = rocprim::make_transform_iterator(rocprim::counting_iterator<uint64_t>(0),
-                                               UnitCount{arena, offsets, lengths, n});
-    if (rocprim::exclusive_scan(tmp, tb, it, unit_start, uint64_t(0), n + 1,
-                                rocprim::plus<uint64_t>(), st) != hipSuccess)
-        return ZDB_CRC32_ELAUNCH;
+    if (!d_unit_start) {
+        uint64_t *us = static_cast<uint64_t *>(w.ptr);
+        void *tmp = static_cast<uint8_t *>(w.ptr) + us_bytes + scratch_bytes;
+        size_t tb = tmp_bytes;
+        auto it = rocprim::make_transform_iterator(rocprim::counting_iterator<uint64_t>(0),
+                                                   UnitCount{arena, offsets, lengths, n});
+        if (rocprim::exclusive_scan(tmp, tb, it, us, uint64_t(0), n + 1, rocprim::plus<uint64_t>(), st) !=
+            hipSuccess)
+            return ZDB_CRC32_ELAUNCH;
+        unit_start = us;
+    }
 
     const KernelVariant &kv = variant();
     const uint32_t grid = (uint32_t)(c.cus * WG_PER_CU);
@@ -983,15 +989,16 @@ int enqueue_batch(DeviceCtx &c, const uint8_t *arena, const uint64_t *offsets, c
 }
 
 struct HostStaging {
-    uint8_t *arena = nullptr;
+    uint8_t *arena = nullptr; // device copy of the caller's arena
     size_t arena_bytes = 0;
-    uint64_t *off = nullptr;
-    uint32_t *len = nullptr;
-    uint32_t *out = nullptr;
+    uint8_t *plan = nullptr;  // device: offsets | lengths | unit_start | out
+    uint8_t *hplan = nullptr; // pinned host mirror of plan
     size_t n_cap = 0;
     hipStream_t st = nullptr;
 };
 HostStaging g_host_staging[64];
+
+size_t plan_bytes(size_t n) { return n * 8 + n * 4 + (n + 1) * 8 + n * 4 + 64; }
 
 } // namespace
 
@@ -1131,29 +1138,50 @@ int zdb_crc32_batch(const uint8_t *arena, size_t arena_len, const uint64_t *offs
         h.arena_bytes = abytes;
     }
     if (h.n_cap < n) {
-        hipFree(h.off);
-        hipFree(h.len);
-        hipFree(h.out);
-        h.off = nullptr;
-        h.len = nullptr;
-        h.out = nullptr;
-        if (hipMalloc(&h.off, n * 8) != hipSuccess || hipMalloc(&h.len, n * 4) != hipSuccess ||
-            hipMalloc(&h.out, n * 4) != hipSuccess) {
+        if (h.plan)
+            hipFree(h.plan);
+        if (h.hplan)
+            hipHostFree(h.hplan);
+        h.plan = nullptr;
+        h.hplan = nullptr;
+        if (hipMalloc(&h.plan, plan_bytes(n)) != hipSuccess ||
+            hipHostMalloc(&h.hplan, plan_bytes(n), hipHostMallocDefault) != hipSuccess) {
             h.n_cap = 0;
             return ZDB_CRC32_ENOMEM;
         }
         h.n_cap = n;
     }
+    // host-side planning: the descriptors and the unit prefix go over in one
+    // copy, so a small batch (one SET value) needs no device scan
+    uint64_t *ho = reinterpret_cast<uint64_t *>(h.hplan);
+    uint32_t *hl = reinterpret_cast<uint32_t *>(h.hplan + n * 8);
+    uint64_t *hu = reinterpret_cast<uint64_t *>(h.hplan + n * 12);
+    uint32_t *hout = reinterpret_cast<uint32_t *>(h.hplan + n * 12 + (n + 1) * 8);
+    std::memcpy(ho, offsets, n * 8);
+    std::memcpy(hl, lengths, n * 4);
+    const UnitCount uc{h.arena, offsets, lengths, n};
+    uint64_t acc = 0;
+    for (size_t r = 0; r < n; r++) {
+        hu[r] = acc;
+        acc += uc(r);
+    }
+    hu[n] = acc;
+    uint64_t *d_off = reinterpret_cast<uint64_t *>(h.plan);
+    uint32_t *d_len = reinterpret_cast<uint32_t *>(h.plan + n * 8);
+    uint64_t *d_us = reinterpret_cast<uint64_t *>(h.plan + n * 12);
+    uint32_t *d_out = reinterpret_cast<uint32_t *>(h.plan + n * 12 + (n + 1) * 8);
     if (hipMemcpyAsync(h.arena, arena, arena_len, hipMemcpyHostToDevice, h.st) != hipSuccess ||
-        hipMemcpyAsync(h.off, offsets, n * 8, hipMemcpyHostToDevice, h.st) != hipSuccess ||
-        hipMemcpyAsync(h.len, lengths, n * 4, hipMemcpyHostToDevice, h.st) != hipSuccess)
+        hipMemcpyAsync(h.plan, h.hplan, n * 12 + (n + 1) * 8, hipMemcpyHostToDevice, h.st) != hipSuccess)
         return ZDB_CRC32_ELAUNCH;
-    rc = enqueue_batch(*c, h.arena, h.off, h.len, h.out, n, h.st);
+    rc = enqueue_batch(*c, h.arena, d_off, d_len, d_out, n, h.st, d_us);
     if (rc)
         return rc;
-    if (hipMemcpyAsync(out, h.out, n * 4, hipMemcpyDeviceToHost, h.st) != hipSuccess)
+    if (hipMemcpyAsync(hout, d_out, n * 4, hipMemcpyDeviceToHost, h.st) != hipSuccess)
         return ZDB_CRC32_ELAUNCH;
-    return hipStreamSynchronize(h.st) == hipSuccess ? ZDB_CRC32_OK : ZDB_CRC32_ELAUNCH;
+    if (hipStreamSynchronize(h.st) != hipSuccess)
+        return ZDB_CRC32_ELAUNCH;
+    std::memcpy(out, hout, n * 4);
+    return ZDB_CRC32_OK;
 }
 
 void *zdb_crc32_host_alloc(size_t bytes) {

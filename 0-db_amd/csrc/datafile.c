@@ -105,3 +105,29 @@ size_t zdb_datafile_payloads(const zdb_record_t *recs, size_t nrecs, uint64_t *o
     }
     return m;
 }
+
+size_t zdb_datafile_encode_batch(uint8_t *dst, size_t cap, uint64_t file_offset, const uint8_t *keys,
+                                 const uint64_t *key_offsets, const uint8_t *key_lengths,
+                                 const uint8_t *values, const uint64_t *value_offsets,
+                                 const uint32_t *value_lengths, const uint32_t *crcs, size_t n,
+                                 uint32_t timestamp, uint32_t *previous, uint64_t *entry_offsets) {
+    size_t pos = 0;
+    uint32_t prev = previous ? *previous : 0;
+    for (size_t i = 0; i < n; i++) {
+        const size_t need = ZDB_ENTRY_HEADER_SIZE + key_lengths[i] + (size_t)value_lengths[i];
+        if (pos + need > cap)
+            return 0;
+        const uint64_t here = file_offset + pos;
+        pos += zdb_datafile_encode_entry(dst + pos, keys + key_offsets[i], key_lengths[i], value_lengths[i],
+                                         prev, crcs[i], 0, timestamp);
+        if (value_lengths[i])
+            memcpy(dst + pos, values + value_offsets[i], value_lengths[i]);
+        pos += value_lengths[i];
+        if (entry_offsets)
+            entry_offsets[i] = here;
+        prev = (uint32_t)here; /* root->previous = offset (data.c:630) */
+    }
+    if (previous)
+        *previous = prev;
+    return pos;
+}

@@ -71,6 +71,8 @@ _walk = _fn("zdb_datafile_walk", C.c_long, vp, C.c_size_t, vp, C.c_long, C.POINT
 _encode_entry = _fn("zdb_datafile_encode_entry", C.c_size_t, vp, vp, C.c_uint8, C.c_uint32, C.c_uint32,
                     C.c_uint32, C.c_uint8, C.c_uint32)
 _encode_header = _fn("zdb_datafile_encode_header", C.c_size_t, vp, C.c_uint32)
+_encode_batch = _fn("zdb_datafile_encode_batch", C.c_size_t, vp, C.c_size_t, C.c_uint64, vp, vp, vp, vp, vp,
+                    vp, vp, C.c_size_t, C.c_uint32, C.POINTER(C.c_uint32), vp)
 
 #: every symbol include/*.h declares (checked by tests/test_abi.py)
 EXPORTED = [
@@ -80,7 +82,7 @@ EXPORTED = [
     "zdb_crc32_batch", "zdb_crc32_host_alloc", "zdb_crc32_host_free", "zdb_crc32_set_timing",
     "zdb_crc32_kernel_stats", "zdb_synth_fill", "zdb_synth_fill_device", "zdb_synth_zipf_lengths",
     "zdb_datafile_walk", "zdb_datafile_encode_entry", "zdb_datafile_encode_header",
-    "zdb_datafile_payloads",
+    "zdb_datafile_payloads", "zdb_datafile_encode_batch",
 ]
 
 RECORD_DTYPE = np.dtype([
@@ -287,3 +289,26 @@ def encode_entry(key: bytes, datalength: int, previous: int, integrity: int, fla
     n = _encode_entry(buf.ctypes.data, k.ctypes.data if k is not None else None, len(key), datalength,
                       previous, integrity, flags, timestamp)
     return buf[:n].tobytes()
+
+
+def encode_batch(keys: list[bytes], values: np.ndarray, value_offsets, value_lengths, crcs, file_offset: int,
+                 previous: int = 0, timestamp: int = 0):
+    """In-order append of n entries (data_insert semantics) -> (bytes, previous, entry_offsets)."""
+    kl = np.array([len(k) for k in keys], dtype=np.uint8)
+    ko = np.zeros(len(keys), dtype=np.uint64)
+    if len(keys) > 1:
+        ko[1:] = np.cumsum(kl[:-1], dtype=np.uint64)
+    kb = np.frombuffer(b"".join(keys) or b"\0", dtype=np.uint8)
+    vo = np.ascontiguousarray(value_offsets, dtype=np.uint64)
+    vl = np.ascontiguousarray(value_lengths, dtype=np.uint32)
+    cr = np.ascontiguousarray(crcs, dtype=np.uint32)
+    cap = int(vl.sum(dtype=np.uint64)) + int(kl.sum()) + 18 * len(keys)
+    out = np.zeros(max(cap, 1), dtype=np.uint8)
+    prev = C.c_uint32(previous)
+    eo = np.zeros(len(keys), dtype=np.uint64)
+    n = _encode_batch(out.ctypes.data, cap, file_offset, kb.ctypes.data, ko.ctypes.data, kl.ctypes.data,
+                      values.ctypes.data, vo.ctypes.data, vl.ctypes.data, cr.ctypes.data, len(keys), timestamp,
+                      C.byref(prev), eo.ctypes.data)
+    if n != cap:
+        raise ZdbCrcError("zdb_datafile_encode_batch: capacity")
+    return out[:n].tobytes(), prev.value, eo

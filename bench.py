@@ -108,6 +108,98 @@ def cpu_baseline(offs, lens, seed, seconds: float) -> dict | None:
             "single_thread_gibs": round(st, 3)}
 
 
+def e2e_legs(offs, lens, seed) -> dict:
+    """Host-memory paths, reported beside the
+    device-resident number: the SET path's 256 KiB value through the
+    host-buffer entry (pinned staging, H2D + kernel + D2H), the zipf batch
+    from pinned host memory (PCIe-inclusive rate), and the integrity-check
+    tool on a 256 MiB datafile (65,000 x 4 KiB, as SURVEY §6) against the
+    reference tool and the scalar engine."""
+    import subprocess
+    import tempfile
+    import oracle
+    import zdbcrc
+    res = {}
+    V = 256 * 1024
+    pin = zdbcrc.PinnedBuffer(64 * V)
+    pin.array[:] = zdbcrc.synth_fill(64 * V, 0xC5)
+    one = pin.array[:V]
+    want = zdbcrc.crc32(one)
+    for _ in range(5):
+        assert zdbcrc.batch_host(one, [0], [V])[0] == want
+    set_path = {}
+    for b in (1, 8, 64):
+        offs_b = np.arange(b, dtype=np.uint64) * V
+        lens_b = np.full(b, V, np.uint32)
+        ts = []
+        for _ in range(50 if b < 64 else 20):
+            t0 = time.perf_counter()
+            zdbcrc.batch_host(pin.array[:b * V], offs_b, lens_b)
+            ts.append(time.perf_counter() - t0)
+        med = float(np.median(ts))
+        set_path[f"batch{b}"] = {"us_per_call": round(med * 1e6, 1), "gibs": round(b * V / med / GIB, 2)}
+    ts = []
+    for _ in range(200):
+        t0 = time.perf_counter()
+        zdbcrc.crc32(one)
+        ts.append(time.perf_counter() - t0)
+    set_path["cpu_scalar_engine_us"] = round(float(np.median(ts)) * 1e6, 1)
+    if oracle.Reference.available():
+        ref = oracle.Reference()
+        ts = []
+        for _ in range(200):
+            t0 = time.perf_counter()
+            ref.crc32(one)
+            ts.append(time.perf_counter() - t0)
+        set_path["cpu_reference_us"] = round(float(np.median(ts)) * 1e6, 1)
+    res["set_path_256KiB"] = set_path
+    pin.free()
+
+    # zipf batch from pinned host memory: PCIe-inclusive
+    total = int(offs[-1] + lens[-1])
+    hp = zdbcrc.PinnedBuffer(total + 16)
+    hp.array[:total + 16] = zdbcrc.synth_fill(total + 16, seed)
+    o, l = offs.astype(np.uint64), lens.astype(np.uint32)
+    zdbcrc.batch_host(hp.array, o, l)
+    ts = []
+    for _ in range(3):
+        t0 = time.perf_counter()
+        zdbcrc.batch_host(hp.array, o, l)
+        ts.append(time.perf_counter() - t0)
+    res["zipf_from_pinned_host"] = {"gibs": round(int(lens.sum()) / min(ts) / GIB, 1),
+                                    "s": round(min(ts), 4)}
+    hp.free()
+
+    # integrity-check on a 256 MiB datafile written through the SET batch path
+    n = 65000
+    vals = zdbcrc.synth_fill(n * 4096, 0xC1)
+    vo = np.arange(n, dtype=np.uint64) * 4096
+    vl = np.full(n, 4096, np.uint32)
+    crcs = zdbcrc.batch_host(vals, vo, vl)  # SET-path batch checksum on the GPU
+    keys = [b"k%d" % i for i in range(n)]
+    body, _, _ = zdbcrc.encode_batch(keys, vals, vo, vl, crcs, file_offset=28)
+    with tempfile.TemporaryDirectory() as td:
+        with open(f"{td}/d0", "wb") as f:
+            f.write(zdbcrc.encode_header(0) + body)
+        os.symlink("d0", f"{td}/zdb-data-0")
+        tools = {"gpu_tool": [str(ROOT / "0-db_amd/bin/zdb-integrity-check"), f"{td}/zdb-data-0"],
+                 "scalar_engine_tool": [str(ROOT / "0-db_amd/bin/zdb-integrity-check"), "--engine=cpu",
+                                        f"{td}/zdb-data-0"]}
+        if oracle.REF_INTEGRITY.exists():
+            tools["reference_tool"] = [str(oracle.REF_INTEGRITY), f"{td}/zdb-data-0"]
+        ic = {"file_bytes": 28 + len(body), "records": n}
+        for name, cmd in tools.items():
+            ts = []
+            for _ in range(3):
+                t0 = time.perf_counter()
+                p = subprocess.run(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, timeout=120)
+                ts.append(time.perf_counter() - t0)
+                assert p.returncode == 0, (name, p.stderr[-500:])
+            ic[name + "_s"] = round(min(ts), 4)
+        res["integrity_check_256MiB"] = ic
+    return res
+
+
 def pmc_traffic(workload: str):
     p = ROOT / "profiles" / "pmc_traffic.json"
     if not p.exists():
@@ -239,6 +331,10 @@ def main():
                         "roofline_frac": round((pb + 16 * len(l2)) / (km / max(kl, 1) / 1e3) / 1e9
                                                / HBM_PEAK_GBS, 4)}
         del a2
+
+    if rank == 0 and world == 1 and not args.no_extra:
+        log("end-to-end legs (host memory)")
+        extra["e2e"] = e2e_legs(offs, lens, seed)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -63,6 +63,22 @@ size_t zdb_datafile_encode_entry(uint8_t *dst, const uint8_t *id, uint8_t idleng
 /* Encode the 28-byte file header (data_initialize, data.c: created/opened 0). */
 size_t zdb_datafile_encode_header(uint8_t *dst, uint32_t fileid);
 
+/* SET-path batching hook (the in-order second phase of a pipelined SET
+ * batch): append n entries to a datafile image at dst (capacity cap bytes),
+ * exactly as n successive data_insert calls would (data.c:594-633): header
+ * with the caller-computed crc (from zdb_crc32_batch*), key, payload;
+ * `previous` chains each entry to the one before, starting from *previous
+ * (the offset of the last entry already in the file), and file_offset is
+ * the offset at which dst will be written.  key i is keys[key_offsets[i] ..
+ * + key_lengths[i]], value i is values[value_offsets[i] .. + value_lengths[i]].
+ * Entry i's file offset is written to entry_offsets[i] (may be NULL) and
+ * *previous is updated.  Returns bytes written, 0 if cap is too small. */
+size_t zdb_datafile_encode_batch(uint8_t *dst, size_t cap, uint64_t file_offset, const uint8_t *keys,
+                                 const uint64_t *key_offsets, const uint8_t *key_lengths,
+                                 const uint8_t *values, const uint64_t *value_offsets,
+                                 const uint32_t *value_lengths, const uint32_t *crcs, size_t n,
+                                 uint32_t timestamp, uint32_t *previous, uint64_t *entry_offsets);
+
 /* Gather descriptors for the batched checksum: records with datalength > 0
  * (integrity-check.c:81-82 skips empty ones).  Returns the count written. */
 size_t zdb_datafile_payloads(const zdb_record_t *recs, size_t nrecs, uint64_t *offsets, uint32_t *lengths,

@@ -161,3 +161,23 @@ def test_deleted_entries_present():
     deleted = recs[recs["flags"] & 1 == 1]
     assert len(deleted) == 2
     assert (deleted["datalength"] == 0).all() and (deleted["integrity"] == 0).all()
+
+
+def test_encode_batch_matches_reference_inserts():
+    """zdb_datafile_encode_batch == successive reference data_insert calls
+    (fixed_4k.d0 was written by libzdb; timestamps are taken from the file)."""
+    img = (GOLDEN / "datafiles" / "fixed_4k.d0").read_bytes()
+    recs, status = zdbcrc.datafile_walk(img)
+    assert status == 0
+    arr = np.frombuffer(img, np.uint8)
+    keys = [img[int(r["header_offset"]) + 18:int(r["payload_offset"])] for r in recs]
+    out, prev, eo = zdbcrc.encode_batch(keys, arr, recs["payload_offset"], recs["datalength"],
+                                        recs["integrity"], file_offset=28, previous=0,
+                                        timestamp=int(recs["timestamp"][0]))
+    got = bytearray(img[:28] + out)
+    for r in recs:  # the reference stamps each insert with time(NULL)
+        h = int(r["header_offset"])
+        got[h + 14:h + 18] = img[h + 14:h + 18]
+    assert bytes(got) == img
+    assert prev == int(recs["header_offset"][-1])
+    np.testing.assert_array_equal(eo, recs["header_offset"])
