@@ -200,6 +200,22 @@ def e2e_legs(offs, lens, seed) -> dict:
     return res
 
 
+def combine_ranks(elapsed_s: float, payload: int, world: int) -> tuple[float, float]:
+    """Whole-job aggregation: the slowest rank's time and the bytes of all
+    ranks (the only cross-rank traffic; the data path has no collective).
+    Works on any initialised backend (nccl on the GPU box, gloo in tests)."""
+    if world == 1:
+        return elapsed_s, float(payload)
+    import torch
+    import torch.distributed as dist
+    dev = "cuda" if dist.get_backend() == "nccl" else "cpu"
+    t = torch.tensor([elapsed_s], dtype=torch.float64, device=dev)
+    b = torch.tensor([float(payload)], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    dist.all_reduce(b, op=dist.ReduceOp.SUM)
+    return float(t.item()), float(b.item())
+
+
 def pmc_traffic(workload: str):
     p = ROOT / "profiles" / "pmc_traffic.json"
     if not p.exists():
@@ -238,13 +254,6 @@ def main():
     def barrier():
         if world > 1:
             dist.barrier()
-
-    def allreduce(x: float, op) -> float:
-        if world == 1:
-            return x
-        t = torch.tensor([x], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=op)
-        return float(t.item())
 
     target = int(args.gib * (1 << 30))
     offs, lens, seed, desc = make_dataset(args.workload, target, rank)
@@ -291,8 +300,7 @@ def main():
     zdbcrc.set_timing(False)
     kern_ms, launches = zdbcrc.kernel_stats()
 
-    elapsed = allreduce(t1 - t0, dist.ReduceOp.MAX if world > 1 else None)
-    all_payload = allreduce(float(payload), dist.ReduceOp.SUM if world > 1 else None)
+    elapsed, all_payload = combine_ranks(t1 - t0, payload, world)
     value = all_payload * args.steps / elapsed / GIB
     ms_per_step = elapsed / args.steps * 1e3
 
