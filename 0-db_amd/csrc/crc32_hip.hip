@@ -620,7 +620,9 @@ __device__ __forceinline__ uint32_t seg_value_v3(const Seg &sg, uint32_t acc, ui
     return x;
 }
 
-template <int WGT, int WPE>
+// STAMP (diagnostic build only): each wave writes its start/end
+// s_memrealtime to scratch[16384 + 4 gw ...] -- never read by the kernel
+template <int WGT, int WPE, bool STAMP = false>
 __global__ __launch_bounds__(WGT, WPE) void crc_batch_kernel_v3(
     const uint8_t *__restrict__ arena, const uint64_t *__restrict__ offsets,
     const uint32_t *__restrict__ lengths, const uint64_t *__restrict__ unit_start, uint64_t n,
@@ -634,6 +636,7 @@ __global__ __launch_bounds__(WGT, WPE) void crc_batch_kernel_v3(
             dst[i] = src[i];
     }
     __syncthreads();
+    const uint64_t t_start = STAMP ? __builtin_amdgcn_s_memrealtime() : 0;
 
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t gw = __builtin_amdgcn_readfirstlane(blockIdx.x * (WGT / 64) + (threadIdx.x >> 6));
@@ -707,6 +710,11 @@ __global__ __launch_bounds__(WGT, WPE) void crc_batch_kernel_v3(
         for (int i = 0; i < K; i++)
             bufc[i] = bufn[i];
     }
+    if (STAMP && lane == 0) {
+        uint64_t *st = reinterpret_cast<uint64_t *>(scratch + 16384) + 2 * gw;
+        st[0] = t_start;
+        st[1] = __builtin_amdgcn_s_memrealtime();
+    }
     if (lane == 0) {
         for (uint32_t i = 0; i < ncut && i < 2; i++)
             atomicXor(out + cut_r[i], cut_x[i]);
@@ -727,6 +735,7 @@ const KernelVariant kVariants[] = {
     {"v3_wg768", crc_batch_kernel_v3<768, 6>, 768},
     {"v3_wg1024", crc_batch_kernel_v3<1024, 8>, 1024},
     {"v3_wg512", crc_batch_kernel_v3<512, 4>, 512},
+    {"v3_wg768_stamp", crc_batch_kernel_v3<768, 6, true>, 768},
     {"wg512_w4_pipe", crc_batch_kernel<512, 4, true>, 512},
     {"wg512_w4", crc_batch_kernel<512, 4, false>, 512},
     {"wg768_w6_pipe", crc_batch_kernel<768, 6, true>, 768},
@@ -868,6 +877,7 @@ struct DeviceCtx {
 };
 
 std::mutex g_mu;
+uint32_t *g_last_scratch = nullptr;
 DeviceCtx g_dev[64];
 bool g_hip_touched = false;
 bool g_timing = false;
@@ -934,7 +944,7 @@ int enqueue_batch(DeviceCtx &c, const uint8_t *arena, const uint64_t *offsets, c
 
     const size_t us_bytes = d_unit_start ? 0 : ((n + 1) * sizeof(uint64_t) + 255) & ~size_t(255);
     const size_t tmp_bytes = d_unit_start ? 0 : scan_temp_bytes(n);
-    const size_t scratch_bytes = 64 * 1024; // one dword per wave of the grid
+    const size_t scratch_bytes = 256 * 1024; // dummy dword per wave + diagnostic stamps
     const size_t need = us_bytes + scratch_bytes + tmp_bytes + 256;
     Workspace &w = c.ws[reinterpret_cast<void *>(st)];
     if (w.bytes < need) {
@@ -950,6 +960,7 @@ int enqueue_batch(DeviceCtx &c, const uint8_t *arena, const uint64_t *offsets, c
     }
     const uint64_t *unit_start = d_unit_start;
     uint32_t *scratch = reinterpret_cast<uint32_t *>(static_cast<uint8_t *>(w.ptr) + us_bytes);
+    g_last_scratch = scratch;
     if (!d_unit_start) {
         uint64_t *us = static_cast<uint64_t *>(w.ptr);
         void *tmp = static_cast<uint8_t *>(w.ptr) + us_bytes + scratch_bytes;
@@ -1052,6 +1063,14 @@ float zdbcrc_debug_stream_read(const void *d_buf, size_t bytes, uint32_t *d_sink
     hipEventDestroy(a);
     hipEventDestroy(b);
     return ms;
+}
+
+// measurement hook: copy the per-wave (start, end) stamps of the last launch
+// of a STAMP variant (waves * 2 u64) to host memory
+int zdbcrc_debug_read_stamps(uint64_t *host, size_t waves) {
+    if (!g_last_scratch || waves > 8192)
+        return -1;
+    return hipMemcpy(host, g_last_scratch + 16384, waves * 16, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
 }
 
 // measurement hook (not part of the public ABI): select a kernel variant for

@@ -35,16 +35,19 @@ sel = [int(x) for x in sys.argv[2].split(",")] if len(sys.argv) > 2 else list(ra
 work = sys.argv[1] if len(sys.argv) > 1 else "zipf"
 ROUNDS, STEPS = 5, 5
 for wl in work.split(","):
-    if wl == "zipf":
+    align = 1
+    if wl in ("zipf", "zipf16"):
         lens = zdbcrc.zipf_lengths(4 << 30, 0xC3C3C3).astype(np.int64)
         seed = 0x5A0DB5EED + 3
+        align = 16 if wl == "zipf16" else 1
     elif wl == "single":
         lens = np.array([(4 << 30) - 16], np.int64); seed = 0x5A0DB5EED
     elif wl == "fixed64k":
         lens = np.full(1 << 16, 65536, np.int64); seed = 0x5A0DB5EED
     else:
         lens = np.full(1 << 20, 4096, np.int64); seed = 0x5A0DB5EED
-    offs = np.zeros(len(lens), np.int64); offs[1:] = np.cumsum(lens[:-1])
+    padded = (lens + align - 1) // align * align
+    offs = np.zeros(len(lens), np.int64); offs[1:] = np.cumsum(padded[:-1])
     total = int(offs[-1] + lens[-1])
     arena = torch.empty(total + 64, dtype=torch.uint8, device="cuda")
     zdbcrc.synth_fill_device(arena, seed)
