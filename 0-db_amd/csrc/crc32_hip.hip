@@ -278,6 +278,7 @@ static_assert(K == 4, "segment_crc unrolls 4 slots");
 // A record segment as the wave walks it (all fields wave-uniform).
 struct Seg {
     SegCtx c;
+    uint64_t us;   // unit index of the record's first piece
     uint64_t r;    // record index
     uint32_t pb;   // one past the segment's last piece (record-relative)
     uint32_t S;    // supersteps in the segment
@@ -305,6 +306,7 @@ __device__ __forceinline__ bool next_seg(uint64_t &r, uint64_t n, uint64_t ub, u
             const uint64_t A = reinterpret_cast<uint64_t>(arena) + offsets[r];
             const uint64_t Aend = A + lengths[r];
             sg.r = r;
+            sg.us = us;
             sg.c.P0 = A & ~15ull;
             sg.c.np = (uint32_t)(ur - us);
             sg.z = (uint32_t)(sg.c.P0 + 16u * (uint64_t)sg.c.np - Aend);
@@ -576,6 +578,7 @@ __device__ __forceinline__ bool next_seg_batched(uint64_t &r, uint64_t n, uint64
             const uint64_t A = readlane64(m.addr, li);
             const uint64_t Aend = A + __builtin_amdgcn_readlane(m.len, li);
             sg.r = r;
+            sg.us = us;
             sg.c.P0 = A & ~15ull;
             sg.c.np = (uint32_t)(ur - us);
             sg.z = (uint32_t)(sg.c.P0 + 16u * (uint64_t)sg.c.np - Aend);
@@ -622,13 +625,20 @@ __device__ __forceinline__ uint32_t seg_value_v3(const Seg &sg, uint32_t acc, ui
 
 // STAMP (diagnostic build only): each wave writes its start/end
 // s_memrealtime to scratch[16384 + 4 gw ...] -- never read by the kernel
-template <int WGT, int WPE, bool STAMP = false>
+// PRIO: waves of a workgroup publish their progress in LDS every other
+// superstep and the slower half raises its issue priority (s_setprio 3).
+// Without it the co-resident waves of a CU finish up to 2x apart (age-ordered
+// arbitration; measured with the STAMP build) and the kernel ends on a tail.
+template <int WGT, int WPE, bool STAMP = false, bool PRIO = false>
 __global__ __launch_bounds__(WGT, WPE) void crc_batch_kernel_v3(
     const uint8_t *__restrict__ arena, const uint64_t *__restrict__ offsets,
     const uint32_t *__restrict__ lengths, const uint64_t *__restrict__ unit_start, uint64_t n,
     uint32_t *__restrict__ out, const uint32_t *__restrict__ tables, uint32_t max_waves,
     uint32_t *__restrict__ scratch) {
-    __shared__ __attribute__((aligned(16))) uint32_t lds[ZDBCRC_LDS_DW];
+    __shared__ __attribute__((aligned(16))) uint32_t lds[ZDBCRC_LDS_DW + 16];
+    uint32_t *const prog = lds + ZDBCRC_LDS_DW; // per-wave progress (PRIO)
+    if (PRIO && threadIdx.x < 16)
+        prog[threadIdx.x] = 0;
     {
         const uint4 *src = reinterpret_cast<const uint4 *>(tables);
         uint4 *dst = reinterpret_cast<uint4 *>(lds);
@@ -668,10 +678,22 @@ __global__ __launch_bounds__(WGT, WPE) void crc_batch_kernel_v3(
     uint32_t *const dummy = scratch + gw;
     uint64_t cut_r[2] = {0, 0};
     uint32_t cut_x[2] = {0, 0}, ncut = 0;
-    uint32_t css = 0, acc = 0;
+    uint32_t css = 0, acc = 0, iter = 0;
+    const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     uint4 bufc[K], bufn[K];
     load_superstep_v3(cur.c, 0, lane, bufc);
     for (;;) {
+        if (PRIO && (++iter & 1) == 0) {
+            const uint32_t mine = (uint32_t)(cur.us + cur.c.pa + 64u * K * css - ub);
+            if (lane == 0)
+                prog[wid] = mine;
+            const uint32_t other = lane < (uint32_t)(WGT / 64) ? prog[lane] : 0u;
+            const uint32_t ahead = (uint32_t)__popcll(__ballot(other > mine));
+            if (ahead >= (uint32_t)(WGT / 128))
+                __builtin_amdgcn_s_setprio(3);
+            else
+                __builtin_amdgcn_s_setprio(0);
+        }
         uint32_t nss = 0;
         bool more = true;
         if (css + 1 < cur.S) {
@@ -710,10 +732,14 @@ __global__ __launch_bounds__(WGT, WPE) void crc_batch_kernel_v3(
         for (int i = 0; i < K; i++)
             bufc[i] = bufn[i];
     }
+    if (PRIO && lane == 0)
+        prog[wid] = 0xFFFFFFFFu; // finished: counts as ahead of everyone
     if (STAMP && lane == 0) {
-        uint64_t *st = reinterpret_cast<uint64_t *>(scratch + 16384) + 2 * gw;
+        uint64_t *st = reinterpret_cast<uint64_t *>(scratch + 16384) + 4 * gw;
         st[0] = t_start;
         st[1] = __builtin_amdgcn_s_memrealtime();
+        st[2] = __builtin_amdgcn_s_getreg(0xF804); // HW_REG_HW_ID: wave/simd/cu/se
+        st[3] = __builtin_amdgcn_s_getreg(0xF814); // HW_REG_XCC_ID
     }
     if (lane == 0) {
         for (uint32_t i = 0; i < ncut && i < 2; i++)
@@ -736,6 +762,8 @@ const KernelVariant kVariants[] = {
     {"v3_wg1024", crc_batch_kernel_v3<1024, 8>, 1024},
     {"v3_wg512", crc_batch_kernel_v3<512, 4>, 512},
     {"v3_wg768_stamp", crc_batch_kernel_v3<768, 6, true>, 768},
+    {"v3_wg768_prio", crc_batch_kernel_v3<768, 6, false, true>, 768},
+    {"v3_wg768_prio_stamp", crc_batch_kernel_v3<768, 6, true, true>, 768},
     {"wg512_w4_pipe", crc_batch_kernel<512, 4, true>, 512},
     {"wg512_w4", crc_batch_kernel<512, 4, false>, 512},
     {"wg768_w6_pipe", crc_batch_kernel<768, 6, true>, 768},
@@ -944,7 +972,7 @@ int enqueue_batch(DeviceCtx &c, const uint8_t *arena, const uint64_t *offsets, c
 
     const size_t us_bytes = d_unit_start ? 0 : ((n + 1) * sizeof(uint64_t) + 255) & ~size_t(255);
     const size_t tmp_bytes = d_unit_start ? 0 : scan_temp_bytes(n);
-    const size_t scratch_bytes = 256 * 1024; // dummy dword per wave + diagnostic stamps
+    const size_t scratch_bytes = 512 * 1024; // dummy dword per wave + diagnostic stamps
     const size_t need = us_bytes + scratch_bytes + tmp_bytes + 256;
     Workspace &w = c.ws[reinterpret_cast<void *>(st)];
     if (w.bytes < need) {
@@ -1070,7 +1098,7 @@ float zdbcrc_debug_stream_read(const void *d_buf, size_t bytes, uint32_t *d_sink
 int zdbcrc_debug_read_stamps(uint64_t *host, size_t waves) {
     if (!g_last_scratch || waves > 8192)
         return -1;
-    return hipMemcpy(host, g_last_scratch + 16384, waves * 16, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+    return hipMemcpy(host, g_last_scratch + 16384, waves * 32, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
 }
 
 // measurement hook (not part of the public ABI): select a kernel variant for

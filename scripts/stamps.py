@@ -9,7 +9,8 @@ sys.path[:0] = [str(ROOT / "0-db_amd")]
 import torch, zdbcrc
 sv = zdbcrc._lib.zdbcrc_debug_set_variant; sv.restype = C.c_char_p; sv.argtypes = [C.c_int]
 rd = zdbcrc._lib.zdbcrc_debug_read_stamps; rd.restype = C.c_int; rd.argtypes = [C.c_void_p, C.c_size_t]
-idx = [i for i in range(20) if sv(i) and sv(i).decode() == "v3_wg768_stamp"][0]
+vname = sys.argv[2] if len(sys.argv) > 2 else "v3_wg768_stamp"
+idx = [i for i in range(20) if sv(i) and sv(i).decode() == vname][0]
 sv(idx)
 for wl in sys.argv[1].split(","):
     if wl == "zipf":
@@ -27,13 +28,29 @@ for wl in sys.argv[1].split(","):
         zdbcrc.batch_device(arena, do, dl, out)
     torch.cuda.synchronize()
     waves = 256 * 2 * 12
-    st = np.zeros(waves * 2, np.uint64)
+    st = np.zeros(waves * 4, np.uint64)
     assert rd(st.ctypes.data, waves) == 0
-    st = st.reshape(-1, 2).astype(np.int64)
+    st = st.reshape(-1, 4).astype(np.int64)
+    gw = np.arange(waves)[st[:, 1] > 0]
     st = st[st[:, 1] > 0]
+    hw, xcc = st[:, 2], st[:, 3] & 0xF
+    cu = (hw >> 8) & 0xF; sh = (hw >> 12) & 1; se = (hw >> 13) & 0x7; simd = (hw >> 4) & 3
+    cukey = xcc * 1000 + se * 100 + sh * 16 + cu
     t0 = st[:, 0].min()
     s_, e_ = (st[:, 0] - t0) / 100.0, (st[:, 1] - t0) / 100.0  # memrealtime = 100 MHz -> us
     dur = e_ - s_
+    block = gw // 12
+    per_cu = {}
+    for k, e in zip(cukey, e_):
+        per_cu.setdefault(int(k), []).append(e)
+    cu_mean = np.array([np.mean(v) for v in per_cu.values()])
+    cu_spread = np.array([np.max(v) - np.min(v) for v in per_cu.values()])
+    per_x = {int(x): round(float(np.mean(e_[xcc == x])), 1) for x in np.unique(xcc)}
+    per_simd_rank = {}
+    print(json.dumps({"cus": len(per_cu), "waves_per_cu": round(len(st) / max(len(per_cu), 1), 1),
+                      "cu_mean_end_us_min_p50_max": [round(float(x), 1) for x in (cu_mean.min(), np.median(cu_mean), cu_mean.max())],
+                      "within_cu_spread_us_p50_max": [round(float(np.median(cu_spread)), 1), round(float(cu_spread.max()), 1)],
+                      "xcd_mean_end_us": per_x}))
     print(json.dumps({"workload": wl, "waves": len(st), "start_us_p50_max": [round(float(np.median(s_)), 1), round(float(s_.max()), 1)],
                       "end_us_p10_p50_p90_max": [round(float(np.percentile(e_, q)), 1) for q in (10, 50, 90, 100)],
                       "dur_us_min_p50_max": [round(float(dur.min()), 1), round(float(np.median(dur)), 1), round(float(dur.max()), 1)]}))
