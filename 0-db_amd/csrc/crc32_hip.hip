@@ -363,7 +363,7 @@ __global__ __launch_bounds__(WGT, WPE) void crc_batch_kernel(
     const uint8_t *__restrict__ arena, const uint64_t *__restrict__ offsets,
     const uint32_t *__restrict__ lengths, const uint64_t *__restrict__ unit_start, uint64_t n,
     uint32_t *__restrict__ out, const uint32_t *__restrict__ tables, uint32_t max_waves,
-    uint32_t *__restrict__ scratch) {
+    uint32_t *__restrict__ scratch, uint32_t epoch) {
     __shared__ __attribute__((aligned(16))) uint32_t lds[ZDBCRC_LDS_DW];
 
     {
@@ -629,12 +629,15 @@ __device__ __forceinline__ uint32_t seg_value_v3(const Seg &sg, uint32_t acc, ui
 // superstep and the slower half raises its issue priority (s_setprio 3).
 // Without it the co-resident waves of a CU finish up to 2x apart (age-ordered
 // arbitration; measured with the STAMP build) and the kernel ends on a tail.
-template <int WGT, int WPE, bool STAMP = false, bool PRIO = false>
+// PRIO 2: the same, across all waves of a CU (both workgroups), through a
+// per-CU board in global memory (8-byte slots tagged with the launch epoch,
+// read one superstep late so the load never stalls)
+template <int WGT, int WPE, bool STAMP = false, int PRIO = 0>
 __global__ __launch_bounds__(WGT, WPE) void crc_batch_kernel_v3(
     const uint8_t *__restrict__ arena, const uint64_t *__restrict__ offsets,
     const uint32_t *__restrict__ lengths, const uint64_t *__restrict__ unit_start, uint64_t n,
     uint32_t *__restrict__ out, const uint32_t *__restrict__ tables, uint32_t max_waves,
-    uint32_t *__restrict__ scratch) {
+    uint32_t *__restrict__ scratch, uint32_t epoch) {
     __shared__ __attribute__((aligned(16))) uint32_t lds[ZDBCRC_LDS_DW + 16];
     uint32_t *const prog = lds + ZDBCRC_LDS_DW; // per-wave progress (PRIO)
     if (PRIO && threadIdx.x < 16)
@@ -680,10 +683,21 @@ __global__ __launch_bounds__(WGT, WPE) void crc_batch_kernel_v3(
     uint32_t cut_x[2] = {0, 0}, ncut = 0;
     uint32_t css = 0, acc = 0, iter = 0;
     const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    uint64_t *board = nullptr;
+    uint32_t slot = 0;
+    uint64_t board_prev = 0;
+    if (PRIO == 2) {
+        const uint32_t hw = __builtin_amdgcn_s_getreg(0xF804);  // HW_REG_HW_ID
+        const uint32_t xcc = __builtin_amdgcn_s_getreg(0xF814) & 7;
+        const uint32_t cu_key = ((xcc * 8 + ((hw >> 13) & 7)) * 2 + ((hw >> 12) & 1)) * 16 + ((hw >> 8) & 15);
+        board = reinterpret_cast<uint64_t *>(scratch + (64 + 448) * 256) + (uint64_t)cu_key * 64;
+        slot = ((hw >> 4) & 3) * 16 + (hw & 15);
+        board_prev = __hip_atomic_load(board + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
     uint4 bufc[K], bufn[K];
     load_superstep_v3(cur.c, 0, lane, bufc);
     for (;;) {
-        if (PRIO && (++iter & 1) == 0) {
+        if (PRIO == 1 && (++iter & 1) == 0) {
             const uint32_t mine = (uint32_t)(cur.us + cur.c.pa + 64u * K * css - ub);
             if (lane == 0)
                 prog[wid] = mine;
@@ -693,6 +707,21 @@ __global__ __launch_bounds__(WGT, WPE) void crc_batch_kernel_v3(
                 __builtin_amdgcn_s_setprio(3);
             else
                 __builtin_amdgcn_s_setprio(0);
+        }
+        if (PRIO == 2) {
+            const uint32_t mine = (uint32_t)(cur.us + cur.c.pa + 64u * K * css - ub);
+            const uint64_t seen = board_prev; // loaded one superstep ago
+            const bool live = (uint32_t)(seen >> 32) == epoch;
+            const uint32_t nlive = (uint32_t)__popcll(__ballot(live));
+            const uint32_t ahead = (uint32_t)__popcll(__ballot(live && (uint32_t)seen > mine));
+            if (2 * ahead >= nlive)
+                __builtin_amdgcn_s_setprio(3);
+            else
+                __builtin_amdgcn_s_setprio(0);
+            if (lane == 0)
+                __hip_atomic_store(board + slot, ((uint64_t)epoch << 32) | mine, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+            board_prev = __hip_atomic_load(board + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         uint32_t nss = 0;
         bool more = true;
@@ -732,8 +761,11 @@ __global__ __launch_bounds__(WGT, WPE) void crc_batch_kernel_v3(
         for (int i = 0; i < K; i++)
             bufc[i] = bufn[i];
     }
-    if (PRIO && lane == 0)
+    if (PRIO == 1 && lane == 0)
         prog[wid] = 0xFFFFFFFFu; // finished: counts as ahead of everyone
+    if (PRIO == 2 && lane == 0)
+        __hip_atomic_store(board + slot, ((uint64_t)epoch << 32) | 0xFFFFFFFFu, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
     if (STAMP && lane == 0) {
         uint64_t *st = reinterpret_cast<uint64_t *>(scratch + 16384) + 4 * gw;
         st[0] = t_start;
@@ -748,12 +780,13 @@ __global__ __launch_bounds__(WGT, WPE) void crc_batch_kernel_v3(
 }
 
 typedef void (*crc_kernel_fn)(const uint8_t *, const uint64_t *, const uint32_t *, const uint64_t *, uint64_t,
-                              uint32_t *, const uint32_t *, uint32_t, uint32_t *);
+                              uint32_t *, const uint32_t *, uint32_t, uint32_t *, uint32_t);
 
 struct KernelVariant {
     const char *name;
     crc_kernel_fn fn;
     int threads;
+    int wgs_per_cu = WG_PER_CU;
 };
 
 // selectable with ZDBCRC_VARIANT=<index> (A/B measurement); 0 is the default
@@ -762,8 +795,11 @@ const KernelVariant kVariants[] = {
     {"v3_wg1024", crc_batch_kernel_v3<1024, 8>, 1024},
     {"v3_wg512", crc_batch_kernel_v3<512, 4>, 512},
     {"v3_wg768_stamp", crc_batch_kernel_v3<768, 6, true>, 768},
-    {"v3_wg768_prio", crc_batch_kernel_v3<768, 6, false, true>, 768},
-    {"v3_wg768_prio_stamp", crc_batch_kernel_v3<768, 6, true, true>, 768},
+    {"v3_wg768_prio", crc_batch_kernel_v3<768, 6, false, 1>, 768},
+    {"v3_wg768_prio_stamp", crc_batch_kernel_v3<768, 6, true, 1>, 768},
+    {"v3_wg1024x1_prio", crc_batch_kernel_v3<1024, 4, false, 1>, 1024, 1},
+    {"v3_wg768_cuprio", crc_batch_kernel_v3<768, 6, false, 2>, 768},
+    {"v3_wg768_cuprio_stamp", crc_batch_kernel_v3<768, 6, true, 2>, 768},
     {"wg512_w4_pipe", crc_batch_kernel<512, 4, true>, 512},
     {"wg512_w4", crc_batch_kernel<512, 4, false>, 512},
     {"wg768_w6_pipe", crc_batch_kernel<768, 6, true>, 768},
@@ -899,6 +935,7 @@ struct Workspace {
 
 struct DeviceCtx {
     bool ready = false;
+    uint32_t epoch = 0; // launch counter (tags the per-CU progress board)
     int cus = 0;
     uint32_t *d_tables = nullptr;
     std::map<void *, Workspace> ws; // per stream
@@ -972,7 +1009,8 @@ int enqueue_batch(DeviceCtx &c, const uint8_t *arena, const uint64_t *offsets, c
 
     const size_t us_bytes = d_unit_start ? 0 : ((n + 1) * sizeof(uint64_t) + 255) & ~size_t(255);
     const size_t tmp_bytes = d_unit_start ? 0 : scan_temp_bytes(n);
-    const size_t scratch_bytes = 512 * 1024; // dummy dword per wave + diagnostic stamps
+    // dummy dword per wave (64 KiB) | diagnostic stamps (256 KiB) | per-CU progress board (1 MiB)
+    const size_t scratch_bytes = (64 + 448 + 1024) * 1024;
     const size_t need = us_bytes + scratch_bytes + tmp_bytes + 256;
     Workspace &w = c.ws[reinterpret_cast<void *>(st)];
     if (w.bytes < need) {
@@ -1002,7 +1040,7 @@ int enqueue_batch(DeviceCtx &c, const uint8_t *arena, const uint64_t *offsets, c
     }
 
     const KernelVariant &kv = variant();
-    const uint32_t grid = (uint32_t)(c.cus * WG_PER_CU);
+    const uint32_t grid = (uint32_t)(c.cus * kv.wgs_per_cu);
     const uint32_t max_waves = grid * (uint32_t)(kv.threads / 64);
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (g_timing) {
@@ -1017,7 +1055,7 @@ int enqueue_batch(DeviceCtx &c, const uint8_t *arena, const uint64_t *offsets, c
         hipEventRecord(e0, st);
     }
     hipLaunchKernelGGL(kv.fn, dim3(grid), dim3(kv.threads), 0, st, arena, offsets, lengths, unit_start, n,
-                       out, c.d_tables, max_waves, scratch);
+                       out, c.d_tables, max_waves, scratch, ++c.epoch);
     if (hipGetLastError() != hipSuccess)
         return ZDB_CRC32_ELAUNCH;
     if (g_timing) {
