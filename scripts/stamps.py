@@ -46,6 +46,19 @@ for wl in sys.argv[1].split(","):
     cu_mean = np.array([np.mean(v) for v in per_cu.values()])
     cu_spread = np.array([np.max(v) - np.min(v) for v in per_cu.values()])
     per_x = {int(x): round(float(np.mean(e_[xcc == x])), 1) for x in np.unique(xcc)}
+    wgs = {}
+    for b, e in zip(block, e_):
+        wgs.setdefault(int(b), []).append(e)
+    wg_spread = np.array([np.max(v) - np.min(v) for v in wgs.values()])
+    wg_mean = {b: np.mean(v) for b, v in wgs.items()}
+    # the two workgroups sharing a CU: difference of their mean end times
+    cu_wgs = {}
+    for b, k in zip(block, cukey):
+        cu_wgs.setdefault(int(k), set()).add(int(b))
+    pair_gap = np.array([abs(wg_mean[min(v)] - wg_mean[max(v)]) for v in cu_wgs.values() if len(v) == 2])
+    print(json.dumps({"within_wg_spread_us_p50_max": [round(float(np.median(wg_spread)), 1), round(float(wg_spread.max()), 1)],
+                      "wg_pair_mean_gap_us_p50_max": [round(float(np.median(pair_gap)), 1) if len(pair_gap) else None,
+                                                      round(float(pair_gap.max()), 1) if len(pair_gap) else None]}))
     per_simd_rank = {}
     print(json.dumps({"cus": len(per_cu), "waves_per_cu": round(len(st) / max(len(per_cu), 1), 1),
                       "cu_mean_end_us_min_p50_max": [round(float(x), 1) for x in (cu_mean.min(), np.median(cu_mean), cu_mean.max())],
