@@ -84,19 +84,8 @@ __device__ __forceinline__ uint32_t piece_slice(const uint4 &v, int c) {
 
 // contribution of one piece in slot I of a superstep: 26 conflict-free
 // lookups, folded three at a time (v_bitop3 xor3) in issue order
-// MODE is a measurement ablation: 0 = real lookups; 1 = same slicing, no
-// LDS (XOR of the addresses); 2 = data only.  Only MODE 0 is a checksum.
-template <int I, int MODE = 0>
+template <int I>
 __device__ __forceinline__ uint32_t piece_contrib(const uint4 &v, const uint32_t *lds) {
-    if (MODE == 2)
-        return v.x ^ v.y ^ v.z ^ v.w;
-    if (MODE == 1) {
-        uint32_t r = 0;
-#pragma unroll
-        for (int c = 0; c < PCH; c++)
-            r ^= (ZDBCRC_OFF_T + (I * PCH + c) * 32 + piece_slice(v, c)) * 4u;
-        return r;
-    }
     const uint32_t *tab = lds + ZDBCRC_OFF_T + I * PCH * 32;
     // 26 lookups folded two per v_bitop3 (three-input XOR)
     uint32_t r = 0;
@@ -168,24 +157,6 @@ struct SegCtx {
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef const __attribute__((address_space(1))) u32x4 global_u32x4;
 
-// piece for step t on this lane; CHECK: lanes before the segment start read
-// nothing (only the first superstep has such lanes)
-template <bool CHECK>
-__device__ __forceinline__ uint4 load_piece(const SegCtx &s, uint32_t t, uint32_t lane) {
-    const int64_t jj = s.base_j + 64 * (int64_t)t + (int64_t)lane;
-    u32x4 v = {0, 0, 0, 0};
-    if (!CHECK || jj >= (int64_t)s.pa)
-        v = *reinterpret_cast<global_u32x4 *>(s.P0 + 16u * (uint64_t)jj);
-    return make_uint4(v.x, v.y, v.z, v.w);
-}
-
-template <bool CHECK>
-__device__ __forceinline__ void load_superstep(const SegCtx &s, uint32_t ss, uint32_t lane, uint4 (&buf)[K]) {
-#pragma unroll
-    for (int i = 0; i < K; i++)
-        buf[i] = load_piece<CHECK>(s, ss * K + i, lane);
-}
-
 // zero the bytes of a piece that lie outside the record (first/last piece
 // only) and whole pieces before the segment (lanes whose load was clamped)
 __device__ __forceinline__ uint4 fix_edges(const SegCtx &s, uint4 v, uint32_t t, uint32_t lane) {
@@ -196,21 +167,6 @@ __device__ __forceinline__ uint4 fix_edges(const SegCtx &s, uint4 v, uint32_t t,
     if (jj < (int64_t)s.pa)
         v = make_uint4(0, 0, 0, 0);
     return v;
-}
-
-// unconditional loads of one superstep: lanes before the segment read the
-// segment's first piece instead (zeroed later by fix_edges), so the VMEM
-// instruction stream is the same on every path and the compiler's counted
-// waits stay exact
-__device__ __forceinline__ void load_superstep_clamped(const SegCtx &s, uint32_t ss, uint32_t lane,
-                                                       uint4 (&buf)[K]) {
-#pragma unroll
-    for (int i = 0; i < K; i++) {
-        int64_t jj = s.base_j + 64 * (int64_t)(ss * K + i) + (int64_t)lane;
-        jj = jj < (int64_t)s.pa ? (int64_t)s.pa : jj;
-        const u32x4 v = *reinterpret_cast<global_u32x4 *>(s.P0 + 16u * (uint64_t)jj);
-        buf[i] = make_uint4(v.x, v.y, v.z, v.w);
-    }
 }
 
 // fix_edges only where the step (64 pieces, wave-uniform range) holds a
@@ -227,7 +183,7 @@ __device__ __forceinline__ uint4 edge_piece(const SegCtx &s, uint4 v, uint32_t t
 // superstep can hold empty leading steps / lanes and the record's first
 // piece; only the last can hold the record's last piece: EDGE enables the
 // checks there, the middle supersteps run without them.
-template <bool EDGE, int MODE = 0>
+template <bool EDGE>
 __device__ __forceinline__ uint32_t superstep(const SegCtx &s, uint32_t acc, const uint4 (&cur)[K], uint32_t ss,
                                               uint32_t t0, uint32_t lane, const uint32_t *lds) {
     if (ss)
@@ -235,7 +191,7 @@ __device__ __forceinline__ uint32_t superstep(const SegCtx &s, uint32_t acc, con
     const uint32_t tb = ss * K;
 #define ZDBCRC_SLOT(I)                                                                   \
     if (!EDGE || tb + I >= t0)                                                           \
-        acc ^= piece_contrib<I, MODE>(EDGE ? edge_piece(s, cur[I], tb + I, lane) : cur[I], lds);
+        acc ^= piece_contrib<I>(EDGE ? edge_piece(s, cur[I], tb + I, lane) : cur[I], lds);
 
     ZDBCRC_SLOT(0)
     ZDBCRC_SLOT(1)
@@ -245,35 +201,7 @@ __device__ __forceinline__ uint32_t superstep(const SegCtx &s, uint32_t acc, con
     return acc;
 }
 
-// CRC (in padded-record space) of pieces [pa, pb) of one record, wave-reduced.
-// Loads run one superstep (4 KiB per wave) ahead of the lookups.
-__device__ __forceinline__ uint32_t segment_crc(const SegCtx &s, uint32_t pb, uint32_t lane,
-                                                const uint32_t *lds) {
-    const uint32_t nps = pb - s.pa;
-    const uint32_t T = (nps + 63u) / 64u;
-    const uint32_t S = (T + K - 1) / K;
-    const uint32_t t0 = S * K - T; // first step holding any piece of the segment
-
-    uint32_t acc = 0;
-    uint4 cur[K], nxt[K];
-    load_superstep<true>(s, 0, lane, cur);
-    if (S == 1)
-        return wave_xor(lane_place(superstep<true>(s, acc, cur, 0, t0, lane, lds), lane, lds));
-    load_superstep<false>(s, 1, lane, nxt);
-    acc = superstep<true>(s, acc, cur, 0, t0, lane, lds);
-    uint32_t ss = 1;
-    for (; ss + 1 < S; ss++) {
-#pragma unroll
-        for (int i = 0; i < K; i++)
-            cur[i] = nxt[i];
-        load_superstep<false>(s, ss + 1, lane, nxt);
-        acc = superstep<false>(s, acc, cur, ss, t0, lane, lds);
-    }
-    acc = superstep<true>(s, acc, nxt, ss, t0, lane, lds);
-    return wave_xor(lane_place(acc, lane, lds));
-}
-
-static_assert(K == 4, "segment_crc unrolls 4 slots");
+static_assert(K == 4, "superstep unrolls 4 slots");
 
 // A record segment as the wave walks it (all fields wave-uniform).
 struct Seg {
@@ -285,229 +213,6 @@ struct Seg {
     uint32_t t0;   // first non-empty step
     uint32_t z;    // zero bytes padding the record's last piece
 };
-
-// Next record segment of this wave's unit slice [ub, ue), starting at record
-// r (advanced past it).  False when the slice is exhausted.
-__device__ __forceinline__ bool next_seg(uint64_t &r, uint64_t n, uint64_t ub, uint64_t ue,
-                                         const uint64_t *__restrict__ unit_start, const uint8_t *arena,
-                                         const uint64_t *__restrict__ offsets,
-                                         const uint32_t *__restrict__ lengths, Seg &sg) {
-    for (;;) {
-        if (r >= n)
-            return false;
-        const uint64_t u0 = unit_start[r];
-        if (u0 >= ue)
-            return false;
-        const uint64_t us = u0 + UNIT_OVH;
-        const uint64_t ur = unit_start[r + 1];
-        const uint64_t s_lo = ub > us ? ub : us;
-        const uint64_t s_hi = ue < ur ? ue : ur;
-        if (s_hi > s_lo) {
-            const uint64_t A = reinterpret_cast<uint64_t>(arena) + offsets[r];
-            const uint64_t Aend = A + lengths[r];
-            sg.r = r;
-            sg.us = us;
-            sg.c.P0 = A & ~15ull;
-            sg.c.np = (uint32_t)(ur - us);
-            sg.z = (uint32_t)(sg.c.P0 + 16u * (uint64_t)sg.c.np - Aend);
-            sg.c.lo0 = (int)(A & 15u);
-            sg.c.hi_last = 16 - (int)sg.z;
-            sg.c.pa = (uint32_t)(s_lo - us);
-            sg.pb = (uint32_t)(s_hi - us);
-            const uint32_t T = (sg.pb - sg.c.pa + 63u) / 64u;
-            sg.S = (T + K - 1) / K;
-            sg.t0 = sg.S * K - T;
-            sg.c.base_j = (int64_t)sg.pb - 64 * (int64_t)sg.S * K;
-            r++;
-            return true;
-        }
-        r++;
-    }
-}
-
-// lane registers -> the segment's contribution to crc(record)
-__device__ __forceinline__ uint32_t seg_value(const Seg &sg, uint32_t acc, uint32_t lane, const uint32_t *lds,
-                                              const uint32_t *__restrict__ tables) {
-    uint32_t x = __builtin_amdgcn_readfirstlane(wave_xor(lane_place(acc, lane, lds)));
-    if (sg.z) // remove the zero bytes that pad the record's last piece
-        x = uniform_shift(x, tables + ZDBCRC_OFF_Z + sg.z * SCH * 32);
-    uint64_t q = sg.c.np - sg.pb; // record pieces after this segment
-    for (int g = 0; q; g++, q >>= 1)
-        if (q & 1)
-            x = uniform_shift(x, tables + ZDBCRC_OFF_G + g * SCH * 32);
-    return x;
-}
-
-// lane registers -> record contribution -> out[r]
-__device__ __forceinline__ void finish_seg(const Seg &sg, uint32_t acc, uint32_t lane, const uint32_t *lds,
-                                           const uint32_t *__restrict__ tables, uint32_t *__restrict__ out) {
-    uint32_t x = __builtin_amdgcn_readfirstlane(wave_xor(lane_place(acc, lane, lds)));
-    if (sg.z) // remove the zero bytes that pad the record's last piece
-        x = uniform_shift(x, tables + ZDBCRC_OFF_Z + sg.z * SCH * 32);
-    uint64_t q = sg.c.np - sg.pb; // record pieces after this segment
-    for (int g = 0; q; g++, q >>= 1)
-        if (q & 1)
-            x = uniform_shift(x, tables + ZDBCRC_OFF_G + g * SCH * 32);
-    if (lane == 0) {
-        if (sg.c.pa == 0 && sg.pb == sg.c.np)
-            out[sg.r] = x;
-        else
-            atomicXor(&out[sg.r], x);
-    }
-}
-
-// WGT threads per workgroup, WPE = minimum waves per SIMD (register budget),
-// PIPE: loads run one superstep ahead across record boundaries too
-template <int WGT, int WPE, bool PIPE, int MODE = 0>
-__global__ __launch_bounds__(WGT, WPE) void crc_batch_kernel(
-    const uint8_t *__restrict__ arena, const uint64_t *__restrict__ offsets,
-    const uint32_t *__restrict__ lengths, const uint64_t *__restrict__ unit_start, uint64_t n,
-    uint32_t *__restrict__ out, const uint32_t *__restrict__ tables, uint32_t max_waves,
-    uint32_t *__restrict__ scratch, uint32_t epoch) {
-    __shared__ __attribute__((aligned(16))) uint32_t lds[ZDBCRC_LDS_DW];
-
-    {
-        const uint4 *src = reinterpret_cast<const uint4 *>(tables);
-        uint4 *dst = reinterpret_cast<uint4 *>(lds);
-        for (int i = threadIdx.x; i < ZDBCRC_LDS_DW / 4; i += WGT)
-            dst[i] = src[i];
-    }
-    __syncthreads();
-
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t gw = __builtin_amdgcn_readfirstlane(blockIdx.x * (WGT / 64) + (threadIdx.x >> 6));
-    const uint64_t total = unit_start[n];
-    uint64_t nwaves = (total + MIN_UNITS_PER_WAVE - 1) / MIN_UNITS_PER_WAVE;
-    if (nwaves > max_waves)
-        nwaves = max_waves;
-    if (gw >= nwaves)
-        return;
-    const uint64_t ub = total * gw / nwaves;
-    const uint64_t ue = total * (gw + 1) / nwaves;
-    if (ub >= ue)
-        return;
-
-    // record containing unit ub: last r with unit_start[r] <= ub
-    uint64_t lo = 0, hi = n;
-    while (hi - lo > 1) {
-        const uint64_t mid = (lo + hi) >> 1;
-        if (unit_start[mid] <= ub)
-            lo = mid;
-        else
-            hi = mid;
-    }
-
-    if (PIPE) {
-        // One stream of supersteps over the slice's segments.  Every
-        // iteration issues the same VMEM sequence -- 4 clamped loads for the
-        // NEXT superstep (of this segment or the next one), then one store --
-        // so the waits the compiler counts are exact and the next loads stay
-        // in flight while the current superstep is folded.  Whole segments
-        // store out[r]; iterations that finish nothing store to the wave's
-        // scratch slot; the (at most two) segments cut by the slice edges are
-        // XORed into out[] after the loop.
-        uint64_t rn = lo;
-        Seg cur, nx;
-        if (!next_seg(rn, n, ub, ue, unit_start, arena, offsets, lengths, cur))
-            return;
-        uint32_t *const dummy = scratch + gw;
-        uint64_t cut_r[2] = {0, 0};
-        uint32_t cut_x[2] = {0, 0}, ncut = 0;
-        uint32_t css = 0, acc = 0;
-        uint4 bufc[K], bufn[K];
-        load_superstep_clamped(cur.c, 0, lane, bufc);
-        for (;;) {
-            uint32_t nss = 0;
-            bool more = true;
-            if (css + 1 < cur.S) {
-                nx = cur;
-                nss = css + 1;
-            } else if (!next_seg(rn, n, ub, ue, unit_start, arena, offsets, lengths, nx)) {
-                more = false;
-                nx = cur; // harmless re-load keeps the VMEM stream uniform
-                nss = css;
-            }
-            load_superstep_clamped(nx.c, nss, lane, bufn);
-            if (css == 0 || css + 1 == cur.S)
-                acc = superstep<true, MODE>(cur.c, acc, bufc, css, cur.t0, lane, lds);
-            else
-                acc = superstep<false, MODE>(cur.c, acc, bufc, css, cur.t0, lane, lds);
-            uint32_t *dst = dummy;
-            uint32_t x = 0;
-            if (css + 1 == cur.S) {
-                x = seg_value(cur, acc, lane, lds, tables);
-                acc = 0;
-                if (cur.c.pa == 0 && cur.pb == cur.c.np) {
-                    dst = out + cur.r;
-                } else {
-                    cut_r[ncut & 1] = cur.r;
-                    cut_x[ncut & 1] = x;
-                    ncut++;
-                }
-            }
-            if (lane == 0)
-                *dst = x;
-            if (!more)
-                break;
-            cur = nx;
-            css = nss;
-#pragma unroll
-            for (int i = 0; i < K; i++)
-                bufc[i] = bufn[i];
-        }
-        if (lane == 0) {
-            for (uint32_t i = 0; i < ncut && i < 2; i++)
-                atomicXor(out + cut_r[i], cut_x[i]);
-        }
-        return;
-    }
-
-    const uint32_t *ztab = tables + ZDBCRC_OFF_Z;
-    const uint32_t *gtab = tables + ZDBCRC_OFF_G;
-
-    for (uint64_t r = lo;; r++) {
-        const uint64_t us = unit_start[r] + UNIT_OVH;
-        const uint64_t ur = unit_start[r + 1];
-        const uint64_t s_lo = ub > us ? ub : us;
-        const uint64_t s_hi = ue < ur ? ue : ur;
-        if (s_hi > s_lo) {
-            SegCtx s;
-            const uint64_t A = reinterpret_cast<uint64_t>(arena) + offsets[r];
-            const uint64_t Aend = A + lengths[r];
-            s.P0 = A & ~15ull;
-            s.np = (uint32_t)(ur - us);
-            // z zero bytes pad the record's last piece
-            const uint32_t z = (uint32_t)(s.P0 + 16u * (uint64_t)s.np - Aend);
-            s.lo0 = (int)(A & 15u);
-            s.hi_last = 16 - (int)z;
-            s.pa = (uint32_t)(s_lo - us);
-            const uint32_t pb = (uint32_t)(s_hi - us);
-            const uint32_t nps = pb - s.pa;
-            const uint32_t S = ((nps + 63u) / 64u + K - 1) / K;
-            s.base_j = (int64_t)pb - 64 * (int64_t)S * K;
-
-            uint32_t x = __builtin_amdgcn_readfirstlane(segment_crc(s, pb, lane, lds));
-
-            // remove the z zero bytes that pad the record's last piece
-            if (z)
-                x = uniform_shift(x, ztab + z * SCH * 32);
-            // shift over the record pieces that follow this segment
-            uint64_t q = s.np - pb;
-            for (int g = 0; q; g++, q >>= 1)
-                if (q & 1)
-                    x = uniform_shift(x, gtab + g * SCH * 32);
-
-            if (lane == 0) {
-                if (s.pa == 0 && pb == s.np)
-                    out[r] = x;
-                else
-                    atomicXor(&out[r], x);
-            }
-        }
-        if (ur >= ue || r + 1 >= n)
-            break;
-    }
-}
 
 // ---------------------------------------------------------------------------
 // v3: pipelined stream + lane-parallel record metadata + DPP reduction
@@ -528,6 +233,24 @@ __device__ __forceinline__ uint32_t wave_xor_scalar(uint32_t x) {
     x ^= __builtin_amdgcn_update_dpp(0u, x, 0x128, 0xF, 0xF, false); // row_ror:8
     return __builtin_amdgcn_readlane(x, 0) ^ __builtin_amdgcn_readlane(x, 16) ^
            __builtin_amdgcn_readlane(x, 32) ^ __builtin_amdgcn_readlane(x, 48);
+}
+
+// record r with unit_start[r] <= b < unit_start[r+1]: 64-way search, one
+// vector load per round (3 rounds for 1e5 records, 4 for 1e6)
+__device__ __forceinline__ uint64_t find_record(const uint64_t *__restrict__ unit_start, uint64_t n, uint64_t b,
+                                                uint32_t lane) {
+    uint64_t lo = 0, hi = n;
+    while (hi - lo > 1) {
+        const uint64_t step = (hi - lo + 63) >> 6;
+        const uint64_t idx = lo + (uint64_t)lane * step;
+        const bool le = idx < hi && unit_start[idx] <= b;
+        const uint64_t mask = __ballot(le);
+        const uint32_t L = 63u - (uint32_t)__clzll(mask);
+        lo += (uint64_t)L * step;
+        const uint64_t h2 = lo + step;
+        hi = h2 < hi ? h2 : hi;
+    }
+    return lo;
 }
 
 // metadata of 64 consecutive records [rb, rb+64), record rb+l on lane l
@@ -616,10 +339,12 @@ __device__ __forceinline__ uint32_t seg_value_v3(const Seg &sg, uint32_t acc, ui
     uint32_t x = wave_xor_scalar(lane_place(acc, lane, lds));
     if (sg.z)
         x = uniform_shift(x, tables + ZDBCRC_OFF_Z + sg.z * SCH * 32);
-    uint64_t q = sg.c.np - sg.pb;
-    for (int g = 0; q; g++, q >>= 1)
-        if (q & 1)
-            x = uniform_shift(x, tables + ZDBCRC_OFF_G + g * SCH * 32);
+    // shift over the record pieces after the segment: one round per nonzero
+    // radix-256 digit (at most 4 dependent table reads, usually 0-2)
+    uint32_t q = sg.c.np - sg.pb;
+    for (int j = 0; q; j++, q >>= 8)
+        if (q & 255u)
+            x = uniform_shift(x, tables + ZDBCRC_OFF_R + (j * 256 + (q & 255u)) * SCH * 32);
     return x;
 }
 
@@ -637,8 +362,34 @@ __global__ __launch_bounds__(WGT, WPE) void crc_batch_kernel_v3(
     uint32_t *__restrict__ scratch, uint32_t epoch) {
     __shared__ __attribute__((aligned(16))) uint32_t lds[ZDBCRC_LDS_DW + 16];
     uint32_t *const prog = lds + ZDBCRC_LDS_DW; // per-wave progress (PRIO)
-    if (PRIO && threadIdx.x < 16)
-        prog[threadIdx.x] = 0;
+    const uint64_t t_start = STAMP ? __builtin_amdgcn_s_memrealtime() : 0;
+
+    // locate this wave's slice and issue its first loads before the table
+    // fill, so the first HBM round trip overlaps the LDS copy; every wave
+    // reaches the barrier below, active or not
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t gw = __builtin_amdgcn_readfirstlane(blockIdx.x * (WGT / 64) + (threadIdx.x >> 6));
+    const uint64_t total = unit_start[n];
+    uint64_t nwaves = (total + MIN_UNITS_PER_WAVE - 1) / MIN_UNITS_PER_WAVE;
+    if (nwaves > max_waves)
+        nwaves = max_waves;
+    const uint64_t ub = total * gw / nwaves;
+    const uint64_t ue = total * (gw + 1) / nwaves;
+    bool active = gw < nwaves && ub < ue;
+    MetaBatch m;
+    uint64_t rn = 0;
+    Seg cur, nx;
+    uint4 bufc[K], bufn[K];
+    if (active) {
+        rn = find_record(unit_start, n, ub, lane);
+        load_meta(m, rn, n, lane, unit_start, arena, offsets, lengths);
+        active = next_seg_batched(rn, n, ub, ue, lane, m, unit_start, arena, offsets, lengths, cur);
+        if (active)
+            load_superstep_v3(cur.c, 0, lane, bufc);
+    }
+    const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    if (PRIO && lane == 0)
+        prog[wid] = active ? 0u : 0xFFFFFFFFu; // an idle wave counts as ahead of everyone
     {
         const uint4 *src = reinterpret_cast<const uint4 *>(tables);
         uint4 *dst = reinterpret_cast<uint4 *>(lds);
@@ -646,42 +397,13 @@ __global__ __launch_bounds__(WGT, WPE) void crc_batch_kernel_v3(
             dst[i] = src[i];
     }
     __syncthreads();
-    const uint64_t t_start = STAMP ? __builtin_amdgcn_s_memrealtime() : 0;
+    if (!active)
+        return;
 
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t gw = __builtin_amdgcn_readfirstlane(blockIdx.x * (WGT / 64) + (threadIdx.x >> 6));
-    const uint64_t total = unit_start[n];
-    uint64_t nwaves = (total + MIN_UNITS_PER_WAVE - 1) / MIN_UNITS_PER_WAVE;
-    if (nwaves > max_waves)
-        nwaves = max_waves;
-    if (gw >= nwaves)
-        return;
-    const uint64_t ub = total * gw / nwaves;
-    const uint64_t ue = total * (gw + 1) / nwaves;
-    if (ub >= ue)
-        return;
-    uint64_t lo = 0, hi = n;
-    while (hi - lo > 1) {
-        const uint64_t mid = (lo + hi) >> 1;
-        if (unit_start[mid] <= ub)
-            lo = mid;
-        else
-            hi = mid;
-    }
-
-    MetaBatch m;
-    load_meta(m, lo, n, lane, unit_start, arena, offsets, lengths);
-    uint64_t rn = lo;
-    Seg cur, nx;
-    if (!next_seg_batched(rn, n, ub, ue, lane, m, unit_start, arena, offsets, lengths, cur))
-        return;
     uint32_t *const dummy = scratch + gw;
     uint64_t cut_r[2] = {0, 0};
     uint32_t cut_x[2] = {0, 0}, ncut = 0;
     uint32_t css = 0, acc = 0, iter = 0;
-    const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    uint4 bufc[K], bufn[K];
-    load_superstep_v3(cur.c, 0, lane, bufc);
     for (;;) {
         if (PRIO == 1 && (++iter & 1) == 0) {
             const uint32_t mine = (uint32_t)(cur.us + cur.c.pa + 64u * K * css - ub);
@@ -747,439 +469,6 @@ __global__ __launch_bounds__(WGT, WPE) void crc_batch_kernel_v3(
     }
 }
 
-// ---------------------------------------------------------------------------
-// v4: dynamic chunk scheduling
-//
-// The static equal-unit slices of v3 leave the kernel waiting on a tail: the
-// co-resident waves of a CU do not progress at the same rate (the sequencer
-// favours older waves), so equal work finishes up to 2x apart.  v4 hands out
-// the unit space in chunks instead: chunk c < P (P = active waves) is wave
-// c's first chunk, the rest are taken from a global counter as waves run out
-// of work.  Chunk sizes follow factoring -- batch j (of P chunks) covers half
-// of what batches < j left over -- down to a minimum chunk, so a wave's first
-// chunks are large (few boundaries) and the end of the kernel drains in
-// small pieces.
-//
-// Chunk edges are snapped, inside a record, to multiples of 256 pieces
-// counted from the record's end: the piece after the edge is np - 256 k.  The
-// partial segment before an edge then needs a shift of exactly k supersteps
-// (G-table bits >= 8 only), the segment after it none, and records of at most
-// 4 KiB are never split.  Both sides of an edge compute the same snap from
-// the edge position alone.
-// ---------------------------------------------------------------------------
-
-constexpr uint64_t V4_MIN_CHUNK = 1024; // units (16 KiB) at full size; power of two
-constexpr uint32_t V4_CTR_DW = (64 + 448) * 256; // scratch dword offset of the chunk counters
-
-struct ChunkPlan {
-    uint64_t T;       // total units
-    uint64_t tail0;   // first unit of the tail region
-    uint64_t nchunks;
-    double inv_p;     // 1 / P
-    uint32_t P;       // active waves
-    uint32_t J;       // factoring batches
-    uint32_t lg_min;  // log2 of the tail chunk size
-};
-
-__device__ __forceinline__ ChunkPlan plan_chunks(uint64_t T, uint32_t P, uint32_t max_waves) {
-    ChunkPlan p;
-    p.T = T;
-    p.P = P;
-    p.inv_p = 1.0 / (double)P;
-    // tail chunk: the largest power of two <= T / max_waves, within [256, V4_MIN_CHUNK]
-    uint32_t lg = 8;
-    while (lg < 10 && ((uint64_t)max_waves << (lg + 1)) <= T)
-        lg++;
-    p.lg_min = lg;
-    uint32_t j = 0;
-    while (j < 32 && (T >> j) - (T >> (j + 1)) >= ((uint64_t)P << lg))
-        j++;
-    p.J = j;
-    p.tail0 = T - (T >> j);
-    p.nchunks = (uint64_t)j * P + (((T >> j) + (1ull << lg) - 1) >> lg);
-    return p;
-}
-
-// [lo, hi) of chunk c; the edges only need to be monotone and computed the
-// same way by both neighbours, so batch chunks use one f64 multiply
-__device__ __forceinline__ uint64_t batch_edge(const ChunkPlan &p, uint32_t j, uint32_t i) {
-    const uint64_t base = p.T - (p.T >> j);
-    const uint64_t D = (p.T >> j) - (p.T >> (j + 1));
-    if (i >= p.P)
-        return base + D;
-    return base + (uint64_t)((double)D * (double)i * p.inv_p);
-}
-
-__device__ __forceinline__ void chunk_range(const ChunkPlan &p, uint64_t c, uint64_t &lo, uint64_t &hi) {
-    const uint64_t jp = (uint64_t)p.J * p.P;
-    if (c < jp) {
-        const uint32_t j = (uint32_t)((double)c * p.inv_p);  // exact: c < 2^40, P < 2^16
-        const uint32_t jj = (uint64_t)j * p.P > c ? j - 1 : ((uint64_t)(j + 1) * p.P <= c ? j + 1 : j);
-        const uint32_t i = (uint32_t)(c - (uint64_t)jj * p.P);
-        lo = batch_edge(p, jj, i);
-        hi = batch_edge(p, jj, i + 1);
-    } else {
-        lo = p.tail0 + ((c - jp) << p.lg_min);
-        hi = lo + (1ull << p.lg_min);
-        hi = hi < p.T ? hi : p.T;
-    }
-}
-
-// record r with unit_start[r] <= b < unit_start[r+1]: 64-way search, one
-// vector load per round (3 rounds for 1e5 records, 4 for 1e6)
-__device__ __forceinline__ uint64_t find_record(const uint64_t *__restrict__ unit_start, uint64_t n, uint64_t b,
-                                                uint32_t lane) {
-    uint64_t lo = 0, hi = n;
-    while (hi - lo > 1) {
-        const uint64_t step = (hi - lo + 63) >> 6;
-        const uint64_t idx = lo + (uint64_t)lane * step;
-        const bool le = idx < hi && unit_start[idx] <= b;
-        const uint64_t mask = __ballot(le);
-        const uint32_t L = 63u - (uint32_t)__clzll(mask);
-        lo += (uint64_t)L * step;
-        const uint64_t h2 = lo + step;
-        hi = h2 < hi ? h2 : hi;
-    }
-    return lo;
-}
-
-// edge b inside record [us, us + np) snapped to np - 256 k (or the record start)
-__device__ __forceinline__ uint64_t snap_edge(uint64_t b, uint64_t us, uint32_t np) {
-    if (b <= us)
-        return us;
-    const uint32_t p = (uint32_t)(b - us);
-    const uint32_t k = (np - p + 255u) >> 8;
-    const int64_t pp = (int64_t)np - 256 * (int64_t)k;
-    return pp > 0 ? us + (uint64_t)pp : us;
-}
-
-// v3's next_seg_batched with snapped chunk edges
-__device__ __forceinline__ bool next_seg_v4(uint64_t &r, uint64_t n, uint64_t ub, uint64_t ue, uint32_t lane,
-                                            MetaBatch &m, const uint64_t *__restrict__ unit_start,
-                                            const uint8_t *arena, const uint64_t *__restrict__ offsets,
-                                            const uint32_t *__restrict__ lengths, Seg &sg) {
-    for (;;) {
-        if (r >= n)
-            return false;
-        if (r >= m.rb + 64)
-            load_meta(m, r, n, lane, unit_start, arena, offsets, lengths);
-        const uint32_t li = (uint32_t)(r - m.rb);
-        const uint64_t u0 = readlane64(m.u0, li);
-        if (u0 >= ue)
-            return false;
-        const uint64_t us = u0 + UNIT_OVH;
-        const uint64_t ur = readlane64(m.ur, li);
-        const uint32_t np = (uint32_t)(ur - us);
-        const uint64_t s_lo = ub > us ? snap_edge(ub, us, np) : us;
-        const uint64_t s_hi = ue < ur ? snap_edge(ue, us, np) : ur;
-        if (s_hi > s_lo) {
-            const uint64_t A = readlane64(m.addr, li);
-            const uint64_t Aend = A + __builtin_amdgcn_readlane(m.len, li);
-            sg.r = r;
-            sg.us = us;
-            sg.c.P0 = A & ~15ull;
-            sg.c.np = np;
-            sg.z = (uint32_t)(sg.c.P0 + 16u * (uint64_t)np - Aend);
-            sg.c.lo0 = (int)(A & 15u);
-            sg.c.hi_last = 16 - (int)sg.z;
-            sg.c.pa = (uint32_t)(s_lo - us);
-            sg.pb = (uint32_t)(s_hi - us);
-            const uint32_t T = (sg.pb - sg.c.pa + 63u) / 64u;
-            sg.S = (T + K - 1) / K;
-            sg.t0 = sg.S * K - T;
-            sg.c.base_j = (int64_t)sg.pb - 64 * (int64_t)sg.S * K;
-            r++;
-            return true;
-        }
-        r++;
-    }
-}
-
-// scratch layout (dwords): [0, 16384) dummy per wave | [16384, ...) stamps |
-// V4_CTR_DW: chunk counter, V4_CTR_DW + 32: finished-wave counter.  The last
-// wave to finish puts both back to 0 for the next launch (the workspace is
-// zeroed when allocated), so replays of a captured graph work too.
-template <int WGT, int WPE, bool STAMP = false>
-__global__ __launch_bounds__(WGT, WPE) void crc_batch_kernel_v4(
-    const uint8_t *__restrict__ arena, const uint64_t *__restrict__ offsets,
-    const uint32_t *__restrict__ lengths, const uint64_t *__restrict__ unit_start, uint64_t n,
-    uint32_t *__restrict__ out, const uint32_t *__restrict__ tables, uint32_t max_waves,
-    uint32_t *__restrict__ scratch, uint32_t epoch) {
-    __shared__ __attribute__((aligned(16))) uint32_t lds[ZDBCRC_LDS_DW];
-    {
-        const uint4 *src = reinterpret_cast<const uint4 *>(tables);
-        uint4 *dst = reinterpret_cast<uint4 *>(lds);
-        for (int i = threadIdx.x; i < ZDBCRC_LDS_DW / 4; i += WGT)
-            dst[i] = src[i];
-    }
-    __syncthreads();
-    const uint64_t t_start = STAMP ? __builtin_amdgcn_s_memrealtime() : 0;
-
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t gw = __builtin_amdgcn_readfirstlane(blockIdx.x * (WGT / 64) + (threadIdx.x >> 6));
-    const uint64_t total = unit_start[n];
-    uint64_t nw = (total + MIN_UNITS_PER_WAVE - 1) / MIN_UNITS_PER_WAVE;
-    const uint32_t P = (uint32_t)(nw < max_waves ? nw : max_waves);
-    if (gw >= P)
-        return;
-    uint32_t *const ctr = scratch + V4_CTR_DW;
-    uint32_t *const fin = scratch + V4_CTR_DW + 32;
-    uint32_t *const dummy = scratch + gw;
-    const ChunkPlan cp = plan_chunks(total, P, max_waves);
-
-    uint64_t c = gw, ub = 0, ue = 0, rn = 0;
-    MetaBatch m;
-    m.rb = ~0ull >> 1;
-    Seg cur, nx;
-    bool have = false;
-    // first non-empty chunk (after snapping a chunk can hold no segment)
-    while (c < cp.nchunks) {
-        chunk_range(cp, c, ub, ue);
-        rn = find_record(unit_start, n, ub, lane);
-        load_meta(m, rn, n, lane, unit_start, arena, offsets, lengths);
-        if (next_seg_v4(rn, n, ub, ue, lane, m, unit_start, arena, offsets, lengths, cur)) {
-            have = true;
-            break;
-        }
-        uint32_t v = 0;
-        if (lane == 0)
-            v = atomicAdd(ctr, 1u);
-        c = (uint64_t)P + __builtin_amdgcn_readfirstlane(v);
-    }
-
-    uint64_t pend_r = ~0ull; // cut record whose partial XOR is held back
-    uint32_t pend_x = 0;
-    if (have) {
-        uint32_t css = 0, acc = 0;
-        uint4 bufc[K], bufn[K];
-        load_superstep_v3(cur.c, 0, lane, bufc);
-        for (;;) {
-            uint32_t nss = 0;
-            bool more = true;
-            if (css + 1 < cur.S) {
-                nx = cur;
-                nss = css + 1;
-            } else {
-                while (!next_seg_v4(rn, n, ub, ue, lane, m, unit_start, arena, offsets, lengths, nx)) {
-                    uint32_t v = 0;
-                    if (lane == 0)
-                        v = atomicAdd(ctr, 1u);
-                    c = (uint64_t)P + __builtin_amdgcn_readfirstlane(v);
-                    if (c >= cp.nchunks) {
-                        more = false;
-                        nx = cur;
-                        nss = css;
-                        break;
-                    }
-                    chunk_range(cp, c, ub, ue);
-                    rn = find_record(unit_start, n, ub, lane);
-                    load_meta(m, rn, n, lane, unit_start, arena, offsets, lengths);
-                }
-            }
-            load_superstep_v3(nx.c, nss, lane, bufn);
-            if (css == 0 || css + 1 == cur.S)
-                acc = superstep<true>(cur.c, acc, bufc, css, cur.t0, lane, lds);
-            else
-                acc = superstep<false>(cur.c, acc, bufc, css, cur.t0, lane, lds);
-            // one atomic XOR per superstep (uniform VMEM stream): a finished
-            // whole record, a flushed cut record, or 0 into the wave's dummy
-            uint32_t *dst = dummy;
-            uint32_t val = 0;
-            if (css + 1 == cur.S) {
-                const uint32_t x = seg_value_v3(cur, acc, lane, lds, tables);
-                acc = 0;
-                if (cur.c.pa == 0 && cur.pb == cur.c.np) {
-                    dst = out + cur.r;
-                    val = x;
-                } else if (cur.r == pend_r) {
-                    pend_x ^= x;
-                } else {
-                    if (pend_r != ~0ull) {
-                        dst = out + pend_r;
-                        val = pend_x;
-                    }
-                    pend_r = cur.r;
-                    pend_x = x;
-                }
-            }
-            if (lane == 0)
-                atomicXor(dst, val);
-            if (!more)
-                break;
-            cur = nx;
-            css = nss;
-#pragma unroll
-            for (int i = 0; i < K; i++)
-                bufc[i] = bufn[i];
-        }
-    }
-    if (STAMP && lane == 0) {
-        uint64_t *st = reinterpret_cast<uint64_t *>(scratch + 16384) + 4 * gw;
-        st[0] = t_start;
-        st[1] = __builtin_amdgcn_s_memrealtime();
-        st[2] = __builtin_amdgcn_s_getreg(0xF804); // HW_REG_HW_ID: wave/simd/cu/se
-        st[3] = __builtin_amdgcn_s_getreg(0xF814); // HW_REG_XCC_ID
-    }
-    if (lane == 0) {
-        if (pend_r != ~0ull)
-            atomicXor(out + pend_r, pend_x);
-        // every counter increment of this wave has returned before this one
-        if (atomicAdd(fin, 1u) == P - 1) {
-            atomicExch(ctr, 0u);
-            atomicExch(fin, 0u);
-        }
-    }
-    (void)epoch;
-}
-
-// ---------------------------------------------------------------------------
-// v5: v3 with a rolling load pipeline -- one K-piece buffer per lane instead
-// of two: slot i's registers take the next superstep's slot-i piece as soon
-// as its slices have been extracted.  Same bytes in flight per wave, 16
-// fewer VGPRs, so 8 waves fit per SIMD (32 per CU) instead of 6.
-// ---------------------------------------------------------------------------
-
-__device__ __forceinline__ uint4 load_slot_v3(const SegCtx &s, uint32_t ss, int i, uint32_t lane) {
-    const uint64_t base = s.P0 + 16u * (uint64_t)s.pa;
-    int32_t rel = (int32_t)(s.base_j - (int64_t)s.pa) + 64 * (int32_t)(ss * K + i) + (int32_t)lane;
-    rel = rel < 0 ? 0 : rel;
-    const u32x4 v = *reinterpret_cast<global_u32x4 *>(base + ((uint64_t)(uint32_t)rel << 4));
-    return make_uint4(v.x, v.y, v.z, v.w);
-}
-
-template <bool EDGE>
-__device__ __forceinline__ uint32_t superstep_roll(const SegCtx &s, uint32_t acc, uint4 (&buf)[K], uint32_t ss,
-                                                   uint32_t t0, uint32_t lane, const uint32_t *lds,
-                                                   const SegCtx &ns, uint32_t nss) {
-    if (ss)
-        acc = advance_superstep(acc, lds);
-    const uint32_t tb = ss * K;
-#define ZDBCRC_RSLOT(I)                                                                               \
-    {                                                                                                 \
-        uint32_t c = 0;                                                                               \
-        if (!EDGE || tb + I >= t0)                                                                    \
-            c = piece_contrib<I>(EDGE ? edge_piece(s, buf[I], tb + I, lane) : buf[I], lds);          \
-        buf[I] = load_slot_v3(ns, nss, I, lane);                                                      \
-        acc ^= c;                                                                                     \
-    }
-    ZDBCRC_RSLOT(0)
-    ZDBCRC_RSLOT(1)
-    ZDBCRC_RSLOT(2)
-    ZDBCRC_RSLOT(3)
-#undef ZDBCRC_RSLOT
-    return acc;
-}
-
-template <int WGT, int WPE, bool STAMP = false, int PRIO = 0>
-__global__ __launch_bounds__(WGT, WPE) void crc_batch_kernel_v5(
-    const uint8_t *__restrict__ arena, const uint64_t *__restrict__ offsets,
-    const uint32_t *__restrict__ lengths, const uint64_t *__restrict__ unit_start, uint64_t n,
-    uint32_t *__restrict__ out, const uint32_t *__restrict__ tables, uint32_t max_waves,
-    uint32_t *__restrict__ scratch, uint32_t epoch) {
-    __shared__ __attribute__((aligned(16))) uint32_t lds[ZDBCRC_LDS_DW + 16];
-    uint32_t *const prog = lds + ZDBCRC_LDS_DW; // per-wave progress (PRIO)
-    if (PRIO && threadIdx.x < 16)
-        prog[threadIdx.x] = 0;
-    {
-        const uint4 *src = reinterpret_cast<const uint4 *>(tables);
-        uint4 *dst = reinterpret_cast<uint4 *>(lds);
-        for (int i = threadIdx.x; i < ZDBCRC_LDS_DW / 4; i += WGT)
-            dst[i] = src[i];
-    }
-    __syncthreads();
-    const uint64_t t_start = STAMP ? __builtin_amdgcn_s_memrealtime() : 0;
-
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t gw = __builtin_amdgcn_readfirstlane(blockIdx.x * (WGT / 64) + (threadIdx.x >> 6));
-    const uint64_t total = unit_start[n];
-    uint64_t nwaves = (total + MIN_UNITS_PER_WAVE - 1) / MIN_UNITS_PER_WAVE;
-    if (nwaves > max_waves)
-        nwaves = max_waves;
-    if (gw >= nwaves)
-        return;
-    const uint64_t ub = total * gw / nwaves;
-    const uint64_t ue = total * (gw + 1) / nwaves;
-    if (ub >= ue)
-        return;
-    const uint64_t lo = find_record(unit_start, n, ub, lane);
-
-    MetaBatch m;
-    load_meta(m, lo, n, lane, unit_start, arena, offsets, lengths);
-    uint64_t rn = lo;
-    Seg cur, nx;
-    if (!next_seg_batched(rn, n, ub, ue, lane, m, unit_start, arena, offsets, lengths, cur))
-        return;
-    uint32_t *const dummy = scratch + gw;
-    uint64_t cut_r[2] = {0, 0};
-    uint32_t cut_x[2] = {0, 0}, ncut = 0;
-    uint32_t css = 0, acc = 0, iter = 0;
-    const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    uint4 buf[K];
-#pragma unroll
-    for (int i = 0; i < K; i++)
-        buf[i] = load_slot_v3(cur.c, 0, i, lane);
-    for (;;) {
-        if (PRIO == 1 && (++iter & 1) == 0) {
-            const uint32_t mine = (uint32_t)(cur.us + cur.c.pa + 64u * K * css - ub);
-            if (lane == 0)
-                prog[wid] = mine;
-            const uint32_t other = lane < (uint32_t)(WGT / 64) ? prog[lane] : 0u;
-            const uint32_t ahead = (uint32_t)__popcll(__ballot(other > mine));
-            if (ahead >= (uint32_t)(WGT / 128))
-                __builtin_amdgcn_s_setprio(3);
-            else
-                __builtin_amdgcn_s_setprio(0);
-        }
-        uint32_t nss = 0;
-        bool more = true;
-        if (css + 1 < cur.S) {
-            nx = cur;
-            nss = css + 1;
-        } else if (!next_seg_batched(rn, n, ub, ue, lane, m, unit_start, arena, offsets, lengths, nx)) {
-            more = false;
-            nx = cur;
-            nss = css;
-        }
-        if (css == 0 || css + 1 == cur.S)
-            acc = superstep_roll<true>(cur.c, acc, buf, css, cur.t0, lane, lds, nx.c, nss);
-        else
-            acc = superstep_roll<false>(cur.c, acc, buf, css, cur.t0, lane, lds, nx.c, nss);
-        uint32_t *dst = dummy;
-        uint32_t x = 0;
-        if (css + 1 == cur.S) {
-            x = seg_value_v3(cur, acc, lane, lds, tables);
-            acc = 0;
-            if (cur.c.pa == 0 && cur.pb == cur.c.np) {
-                dst = out + cur.r;
-            } else {
-                cut_r[ncut & 1] = cur.r;
-                cut_x[ncut & 1] = x;
-                ncut++;
-            }
-        }
-        if (lane == 0)
-            *dst = x;
-        if (!more)
-            break;
-        cur = nx;
-        css = nss;
-    }
-    if (PRIO == 1 && lane == 0)
-        prog[wid] = 0xFFFFFFFFu;
-    if (STAMP && lane == 0) {
-        uint64_t *st = reinterpret_cast<uint64_t *>(scratch + 16384) + 4 * gw;
-        st[0] = t_start;
-        st[1] = __builtin_amdgcn_s_memrealtime();
-        st[2] = __builtin_amdgcn_s_getreg(0xF804);
-        st[3] = __builtin_amdgcn_s_getreg(0xF814);
-    }
-    if (lane == 0) {
-        for (uint32_t i = 0; i < ncut && i < 2; i++)
-            atomicXor(out + cut_r[i], cut_x[i]);
-    }
-    (void)epoch;
-}
-
 typedef void (*crc_kernel_fn)(const uint8_t *, const uint64_t *, const uint32_t *, const uint64_t *, uint64_t,
                               uint32_t *, const uint32_t *, uint32_t, uint32_t *, uint32_t);
 
@@ -1193,24 +482,9 @@ struct KernelVariant {
 // selectable with ZDBCRC_VARIANT=<index> (A/B measurement); 0 is the default
 const KernelVariant kVariants[] = {
     {"v3_wg768_prio", crc_batch_kernel_v3<768, 6, false, 1>, 768},
-    {"v5_wg1024_prio", crc_batch_kernel_v5<1024, 8, false, 1>, 1024},
-    {"v5_wg1024", crc_batch_kernel_v5<1024, 8>, 1024},
-    {"v5_wg768_prio", crc_batch_kernel_v5<768, 6, false, 1>, 768},
-    {"v5_wg1024_prio_stamp", crc_batch_kernel_v5<1024, 8, true, 1>, 1024},
-    {"v4_wg768", crc_batch_kernel_v4<768, 6>, 768},
-    {"v4_wg768_stamp", crc_batch_kernel_v4<768, 6, true>, 768},
     {"v3_wg768", crc_batch_kernel_v3<768, 6>, 768},
-    {"v3_wg1024", crc_batch_kernel_v3<1024, 8>, 1024},
-    {"v3_wg512", crc_batch_kernel_v3<512, 4>, 512},
-    {"v3_wg768_stamp", crc_batch_kernel_v3<768, 6, true>, 768},
     {"v3_wg768_prio_stamp", crc_batch_kernel_v3<768, 6, true, 1>, 768},
-    {"v3_wg1024x1_prio", crc_batch_kernel_v3<1024, 4, false, 1>, 1024, 1},
-    {"wg512_w4_pipe", crc_batch_kernel<512, 4, true>, 512},
-    {"wg512_w4", crc_batch_kernel<512, 4, false>, 512},
-    {"wg768_w6_pipe", crc_batch_kernel<768, 6, true>, 768},
-    {"wg1024_w8_pipe", crc_batch_kernel<1024, 8, true>, 1024},
-    {"ablate_nolds", crc_batch_kernel<1024, 8, true, 1>, 1024},
-    {"ablate_loadonly", crc_batch_kernel<1024, 8, true, 2>, 1024},
+    {"v3_wg768_stamp", crc_batch_kernel_v3<768, 6, true>, 768},
 };
 
 constexpr int kNumVariants = (int)(sizeof(kVariants) / sizeof(kVariants[0]));
@@ -1409,6 +683,8 @@ size_t scan_temp_bytes(uint64_t n) {
 // (host-planned batches); nullptr -> computed on the device by the scan
 int enqueue_batch(DeviceCtx &c, const uint8_t *arena, const uint64_t *offsets, const uint32_t *lengths,
                   uint32_t *out, uint64_t n, hipStream_t st, const uint64_t *d_unit_start = nullptr) {
+    if (n > 0xFFFFFFFFull) // record indices are 32-bit on the device (cut lists, mismatch indices)
+        return ZDB_CRC32_EINVAL;
     if (hipMemsetAsync(out, 0, n * sizeof(uint32_t), st) != hipSuccess)
         return ZDB_CRC32_ELAUNCH;
 

@@ -128,9 +128,12 @@ void zdbcrc_build_tables(uint32_t *img) {
             for (uint32_t v = 0; v < 32; v++)
                 img[ZDBCRC_OFF_Z + (z * ZDBCRC_SCH + c) * 32 + v] = zdbcrc_shift(reg_slice(v, c), -z);
 
-    for (int g = 0; g < ZDBCRC_GBITS; g++)
-        for (int c = 0; c < ZDBCRC_SCH; c++)
-            for (uint32_t v = 0; v < 32; v++)
-                img[ZDBCRC_OFF_G + (g * ZDBCRC_SCH + c) * 32 + v] =
-                    zdbcrc_shift(reg_slice(v, c), (int64_t)16 << g);
+    for (int j = 0; j < ZDBCRC_RDIG; j++)
+        for (uint32_t d = 0; d < 256; d++) {
+            const uint32_t m = xpow((uint64_t)d << (8 * j + 7), 0); /* x^(8 * 16 * d * 256^j) */
+            for (int c = 0; c < ZDBCRC_SCH; c++)
+                for (uint32_t v = 0; v < 32; v++)
+                    img[ZDBCRC_OFF_R + ((j * 256 + d) * ZDBCRC_SCH + c) * 32 + v] =
+                        multmodp(m, reg_slice(v, c));
+        }
 }

@@ -42,7 +42,7 @@ uint32_t zdbcrc_update_bytes(uint32_t crc, const uint8_t *p, size_t n);
 #define ZDBCRC_PCH      26   /* 5-bit slices of a 128-bit piece (25x5+3)  */
 #define ZDBCRC_SCH       7   /* 5-bit slices of a 32-bit register (6x5+2) */
 #define ZDBCRC_WAVE     64
-#define ZDBCRC_GBITS    32   /* generic shift tables: 16 * 2^i bytes       */
+#define ZDBCRC_RDIG      4   /* radix-256 digits of a piece count (< 2^32) */
 
 /* dword offsets inside the image */
 #define ZDBCRC_OFF_T    0                                              /* [K][PCH][32]      */
@@ -50,8 +50,8 @@ uint32_t zdbcrc_update_bytes(uint32_t crc, const uint8_t *p, size_t n);
 #define ZDBCRC_OFF_L    (ZDBCRC_OFF_W + ZDBCRC_SCH * 32)               /* [SCH][32][64]     */
 #define ZDBCRC_LDS_DW   (ZDBCRC_OFF_L + ZDBCRC_SCH * 32 * ZDBCRC_WAVE) /* end of LDS image  */
 #define ZDBCRC_OFF_Z    ZDBCRC_LDS_DW                                  /* [16][SCH][32]     */
-#define ZDBCRC_OFF_G    (ZDBCRC_OFF_Z + 16 * ZDBCRC_SCH * 32)          /* [GBITS][SCH][32]  */
-#define ZDBCRC_TABLE_DW (ZDBCRC_OFF_G + ZDBCRC_GBITS * ZDBCRC_SCH * 32)
+#define ZDBCRC_OFF_R    (ZDBCRC_OFF_Z + 16 * ZDBCRC_SCH * 32)          /* [RDIG][256][SCH][32] */
+#define ZDBCRC_TABLE_DW (ZDBCRC_OFF_R + ZDBCRC_RDIG * 256 * ZDBCRC_SCH * 32)
 
 /*
  * T[i][c][v] : crc of a 16-byte piece whose only set bits are v << 5c,
@@ -59,7 +59,8 @@ uint32_t zdbcrc_update_bytes(uint32_t crc, const uint8_t *p, size_t n);
  * W[c][v]    : shift(v << 5c, 1024*K)          (register across a superstep)
  * L[c][v][l] : shift(v << 5c, 16*(63-l))       (lane l's final placement)
  * Z[z][c][v] : shift(v << 5c, -z), z = 0..15   (trailing pad removal)
- * G[i][c][v] : shift(v << 5c, 16 << i)         (generic shift by pieces)
+ * R[j][d][c][v] : shift(v << 5c, 16 * d * 256^j) (shift by a piece count,
+ *              one radix-256 digit per table: at most 4 dependent rounds)
  */
 void zdbcrc_build_tables(uint32_t *image /* ZDBCRC_TABLE_DW dwords */);
 

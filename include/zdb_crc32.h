@@ -75,7 +75,7 @@ int zdb_crc32_gpu_initialized(void);
  * point of the call.  Records may start and end at any byte alignment and may
  * overlap; lengths may be 0 (crc 0).  The arena must stay readable up to the
  * 16-byte boundary that follows each record's last byte (true for any
- * allocation from hipMalloc). */
+ * allocation from hipMalloc).  n < 2^32 (ZDB_CRC32_EINVAL otherwise). */
 int zdb_crc32_batch_device(const uint8_t *d_arena, const uint64_t *d_offsets,
                            const uint32_t *d_lengths, uint32_t *d_out,
                            size_t n, void *stream);

@@ -3,7 +3,7 @@
 round, every variant runs STEPS batches of the same device-resident dataset;
 reports median/min kernel ms per variant and checks each variant's output
 against variant 0 bit for bit."""
-import ctypes as C, json, sys, time
+import ctypes as C, json, os, sys, time
 from pathlib import Path
 import numpy as np
 ROOT = Path(__file__).resolve().parents[1]
@@ -23,29 +23,36 @@ while True:
 probe = zdbcrc._lib.zdbcrc_debug_stream_read
 probe.restype = C.c_float
 probe.argtypes = [C.c_void_p, C.c_size_t, C.c_void_p, C.c_int, C.c_void_p]
-buf = torch.empty(4 << 30, dtype=torch.uint8, device="cuda"); buf.fill_(7)
 sink = torch.zeros(1 << 16, dtype=torch.int32, device="cuda")
 st = torch.cuda.current_stream().cuda_stream
-for blocks in (2048, 8192, 16384, -4, -8, -16):
-    ts = [probe(buf.data_ptr(), buf.numel(), sink.data_ptr(), blocks, st) for _ in range(6)][1:]
-    print(json.dumps({"probe": "stream_read_4GiB", "blocks": blocks, "median_ms": round(float(np.median(ts)), 4),
-                      "tbs": round(buf.numel() / (np.median(ts) / 1e3) / 1e12, 3)}), flush=True)
-del buf
+for mib in [int(x) for x in os.environ.get("PROBE_MIB", "4096").split(",") if x]:
+    buf = torch.empty(mib << 20, dtype=torch.uint8, device="cuda"); buf.fill_(7)
+    for blocks in (2048, 8192, 16384, -4, -8, -16):
+        ts = [probe(buf.data_ptr(), buf.numel(), sink.data_ptr(), blocks, st) for _ in range(6)][1:]
+        print(json.dumps({"probe": "stream_read_%dMiB" % mib, "blocks": blocks,
+                          "median_ms": round(float(np.median(ts)), 4),
+                          "tbs": round(buf.numel() / (np.median(ts) / 1e3) / 1e12, 3)}), flush=True)
+    del buf
 sel = [int(x) for x in sys.argv[2].split(",")] if len(sys.argv) > 2 else list(range(len(names)))
 work = sys.argv[1] if len(sys.argv) > 1 else "zipf"
 ROUNDS, STEPS = 5, 5
 for wl in work.split(","):
     align = 1
+    size = 4 << 30
+    label = wl
+    if "@" in wl:  # e.g. single@128: the same workload scaled to 128 MiB (cache-resident probe)
+        wl, mib = wl.split("@")
+        size = int(mib) << 20
     if wl in ("zipf", "zipf16"):
-        lens = zdbcrc.zipf_lengths(4 << 30, 0xC3C3C3).astype(np.int64)
+        lens = zdbcrc.zipf_lengths(size, 0xC3C3C3).astype(np.int64)
         seed = 0x5A0DB5EED + 3
         align = 16 if wl == "zipf16" else 1
     elif wl == "single":
-        lens = np.array([(4 << 30) - 16], np.int64); seed = 0x5A0DB5EED
+        lens = np.array([size - 16], np.int64); seed = 0x5A0DB5EED
     elif wl == "fixed64k":
         lens = np.full(1 << 16, 65536, np.int64); seed = 0x5A0DB5EED
     else:
-        lens = np.full(1 << 20, 4096, np.int64); seed = 0x5A0DB5EED
+        lens = np.full(size >> 12, 4096, np.int64); seed = 0x5A0DB5EED
     padded = (lens + align - 1) // align * align
     offs = np.zeros(len(lens), np.int64); offs[1:] = np.cumsum(padded[:-1])
     total = int(offs[-1] + lens[-1])
@@ -68,7 +75,7 @@ for wl in work.split(","):
     for v in sel:
         t = np.array(times[v])
         same = bool(torch.equal(outs[v].cpu(), ref))
-        print(json.dumps({"workload": wl, "variant": names[v], "median_ms": round(float(np.median(t)), 4),
+        print(json.dumps({"workload": label, "variant": names[v], "median_ms": round(float(np.median(t)), 4),
                           "min_ms": round(float(t.min()), 4),
                           "gibs_median": round(payload / (np.median(t) / 1e3) / 2**30, 1),
                           "frac_spec": round((payload + 16 * len(lens)) / (np.median(t) / 1e3) / 8e12, 4),

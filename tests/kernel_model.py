@@ -16,9 +16,9 @@ OFF_W = OFF_T + K * PCH * 32
 OFF_L = OFF_W + SCH * 32
 LDS_DW = OFF_L + SCH * 32 * WAVE
 OFF_Z = LDS_DW
-OFF_G = OFF_Z + 16 * SCH * 32
-GBITS = 32
-TABLE_DW = OFF_G + GBITS * SCH * 32
+OFF_R = OFF_Z + 16 * SCH * 32
+RDIG = 4
+TABLE_DW = OFF_R + RDIG * 256 * SCH * 32
 UNIT_OVH = 16
 MIN_UNITS_PER_WAVE = 256
 
@@ -45,6 +45,17 @@ def _uniform_shift(x: int, tab: np.ndarray, base: int) -> int:
     for c in range(SCH):
         r ^= int(tab[base + c * 32 + ((x >> (5 * c)) & 31)])
     return r
+
+
+def shift_pieces(x: int, q: int, tab: np.ndarray) -> int:
+    """x shifted over q pieces: one radix-256 digit per table (seg_value_v3)."""
+    j = 0
+    while q:
+        if q & 255:
+            x = _uniform_shift(x, tab, OFF_R + (j * 256 + (q & 255)) * SCH * 32)
+        q >>= 8
+        j += 1
+    return x
 
 
 def _keep_mask(lo: int, hi: int, k: int) -> int:
@@ -135,122 +146,9 @@ def batch(arena: np.ndarray, offsets, lengths, tab: np.ndarray, max_waves: int =
                 x = segment_crc(mem, mem_base, P0, pa, pb, np_, a & 15, 16 - z, tab)
                 if z:
                     x = _uniform_shift(x, tab, OFF_Z + z * SCH * 32)
-                q, g = np_ - pb, 0
-                while q:
-                    if q & 1:
-                        x = _uniform_shift(x, tab, OFF_G + g * SCH * 32)
-                    q >>= 1
-                    g += 1
+                x = shift_pieces(x, np_ - pb, tab)
                 out[r] ^= np.uint32(x)  # store for whole records == xor into 0
             if ur >= ue or r + 1 >= n:
                 break
             r += 1
-    return out
-
-
-# ------------------------------------------------------------------ v4 -------
-# dynamic chunk schedule of crc_batch_kernel_v4 (plan_chunks / chunk_range /
-# snap_edge / next_seg_v4 in crc32_hip.hip)
-
-V4_MIN_CHUNK_LG = 10
-
-
-def plan_chunks(T: int, P: int, max_waves: int) -> dict:
-    lg = 8
-    while lg < V4_MIN_CHUNK_LG and (max_waves << (lg + 1)) <= T:
-        lg += 1
-    j = 0
-    while j < 32 and (T >> j) - (T >> (j + 1)) >= (P << lg):
-        j += 1
-    return {"T": T, "P": P, "inv_p": 1.0 / P, "lg": lg, "J": j, "tail0": T - (T >> j),
-            "nchunks": j * P + (((T >> j) + (1 << lg) - 1) >> lg)}
-
-
-def _batch_edge(p: dict, j: int, i: int) -> int:
-    base = p["T"] - (p["T"] >> j)
-    D = (p["T"] >> j) - (p["T"] >> (j + 1))
-    if i >= p["P"]:
-        return base + D
-    return base + int(float(D) * float(i) * p["inv_p"])
-
-
-def chunk_range(p: dict, c: int) -> tuple[int, int]:
-    jp = p["J"] * p["P"]
-    if c < jp:
-        j = int(float(c) * p["inv_p"])
-        if j * p["P"] > c:
-            j -= 1
-        elif (j + 1) * p["P"] <= c:
-            j += 1
-        i = c - j * p["P"]
-        return _batch_edge(p, j, i), _batch_edge(p, j, i + 1)
-    lo = p["tail0"] + ((c - jp) << p["lg"])
-    return lo, min(lo + (1 << p["lg"]), p["T"])
-
-
-def snap_edge(b: int, us: int, np_: int) -> int:
-    if b <= us:
-        return us
-    k = (np_ - (b - us) + 255) >> 8
-    pp = np_ - 256 * k
-    return us + pp if pp > 0 else us
-
-
-def v4_segments(unit_start: np.ndarray, max_waves: int, order=None):
-    """Yield (chunk, record, pa, pb, np) for every segment of the v4 walk,
-    chunks visited in `order` (any permutation: the result must not depend on it)."""
-    n = len(unit_start) - 1
-    T = int(unit_start[n])
-    P = min(max_waves, (T + MIN_UNITS_PER_WAVE - 1) // MIN_UNITS_PER_WAVE)
-    p = plan_chunks(T, P, max_waves)
-    chunks = range(p["nchunks"]) if order is None else order(p["nchunks"])
-    for c in chunks:
-        ub, ue = chunk_range(p, c)
-        r = int(np.searchsorted(unit_start, ub, side="right") - 1)
-        while r < n:
-            u0 = int(unit_start[r])
-            if u0 >= ue:
-                break
-            us, ur = u0 + UNIT_OVH, int(unit_start[r + 1])
-            np_ = ur - us
-            s_lo = snap_edge(ub, us, np_) if ub > us else us
-            s_hi = snap_edge(ue, us, np_) if ue < ur else ur
-            if s_hi > s_lo:
-                yield c, r, s_lo - us, s_hi - us, np_
-            r += 1
-
-
-def batch_v4(arena: np.ndarray, offsets, lengths, tab: np.ndarray, max_waves: int = 4096,
-             base_addr: int = 0, seed: int | None = None) -> np.ndarray:
-    """out[r] as crc_batch_kernel_v4 computes it (chunks in a random order)."""
-    offsets = np.asarray(offsets, dtype=np.int64)
-    lengths = np.asarray(lengths, dtype=np.int64)
-    n = len(offsets)
-    out = np.zeros(n, dtype=np.uint32)
-    if n == 0:
-        return out
-    pad_lo = (base_addr & 15) + 16
-    mem = np.zeros(pad_lo + len(arena) + 32, dtype=np.uint8)
-    mem[pad_lo:pad_lo + len(arena)] = arena
-    mem_base = base_addr - pad_lo
-    A = base_addr + offsets
-    units = np.where(lengths > 0, ((A + lengths - 1) >> 4) - (A >> 4) + 1, 0) + UNIT_OVH
-    unit_start = np.zeros(n + 1, dtype=np.int64)
-    unit_start[1:] = np.cumsum(units)
-    rng = np.random.default_rng(seed)
-    order = None if seed is None else (lambda m: rng.permutation(m))
-    for _, r, pa, pb, np_ in v4_segments(unit_start, max_waves, order):
-        a = int(A[r])
-        P0 = a & ~15
-        z = P0 + 16 * np_ - (a + int(lengths[r]))
-        x = segment_crc(mem, mem_base, P0, pa, pb, np_, a & 15, 16 - z, tab)
-        if z:
-            x = _uniform_shift(x, tab, OFF_Z + z * SCH * 32)
-        q, g = np_ - pb, 0
-        while q:
-            if q & 1:
-                x = _uniform_shift(x, tab, OFF_G + g * SCH * 32)
-            q >>= 1
-            g += 1
-        out[r] ^= np.uint32(x)
     return out

@@ -63,51 +63,9 @@ def test_multi_superstep_record(oracle_c, tab):
         np.testing.assert_array_equal(got, oracle_c.batch(arena, offs, lens))
 
 
-# ------------------------------------------------------------------ v4 -------
-
-@pytest.mark.parametrize("max_waves,seed", [(4096, 1), (5, 2), (2, 3), (64, 4)])
-def test_v4_random_geometries(oracle_c, tab, max_waves, seed):
-    arena, offs, lens = _case(max_waves * 13 + seed, 24, 20_000, 80_000)
-    got = km.batch_v4(arena, offs, lens, tab, max_waves=max_waves, base_addr=seed, seed=seed)
-    np.testing.assert_array_equal(got, oracle_c.batch(arena, offs, lens))
-
-
-def test_v4_split_large_record(oracle_c, tab):
-    arena = oracle.splitmix_bytes(300_000, 5)
-    offs, lens = [7, 0, 299_000], [290_000, 100, 1000]
-    for mw in (3, 17, 4096):
-        got = km.batch_v4(arena, offs, lens, tab, max_waves=mw, base_addr=9, seed=mw)
-        np.testing.assert_array_equal(got, oracle_c.batch(arena, offs, lens))
-
-
-@pytest.mark.parametrize("kind", ["zipf", "fixed4k", "single", "tiny"])
-def test_v4_partition_exact(kind):
-    """Every piece of every record is in exactly one chunk segment, at the
-    full-size wave count; edges inside a record fall on np - 256 k."""
-    if kind == "zipf":
-        lens = zdbcrc.zipf_lengths(512 << 20, 0xC3C3C3)
-    elif kind == "fixed4k":
-        lens = np.full(131_072, 4096)
-    elif kind == "single":
-        lens = np.array([1 << 30])
-    else:
-        lens = np.arange(1, 200) % 7
-    lens = np.asarray(lens, dtype=np.int64)
-    offs = np.concatenate([[0], np.cumsum(lens)[:-1]]) + 3
-    A = offs
-    units = np.where(lens > 0, ((A + lens - 1) >> 4) - (A >> 4) + 1, 0) + km.UNIT_OVH
-    us = np.zeros(len(lens) + 1, dtype=np.int64)
-    us[1:] = np.cumsum(units)
-    covered = np.zeros(len(lens), dtype=np.int64)
-    last_pb = np.zeros(len(lens), dtype=np.int64)
-    nseg = 0
-    for _, r, pa, pb, np_ in km.v4_segments(us, 6144):
-        assert pa == last_pb[r], (r, pa, last_pb[r])  # chunks visit a record in order, no gap/overlap
-        assert (np_ - pb) % 256 == 0 and (pa == 0 or (np_ - pa) % 256 == 0)
-        if np_ <= 256:
-            assert pa == 0 and pb == np_
-        last_pb[r] = pb
-        covered[r] += pb - pa
-        nseg += 1
-    np.testing.assert_array_equal(covered, units - km.UNIT_OVH)
-    assert nseg >= int((lens > 0).sum())
+def test_radix_shift_tables(tab):
+    """R[j][d] tables == zdb_crc32_shift by 16 * d * 256^j bytes."""
+    rng = np.random.default_rng(8)
+    for q in [1, 255, 256, 257, 65535, 65536, 1 << 24, (1 << 28) + 1, 0xFFFFFFFF]:
+        x = int(rng.integers(1, 1 << 32))
+        assert km.shift_pieces(x, q, tab) == zdbcrc.shift(x, 16 * q)
