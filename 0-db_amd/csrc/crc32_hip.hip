@@ -55,7 +55,11 @@ constexpr int K = ZDBCRC_K;
 constexpr int PCH = ZDBCRC_PCH;
 constexpr int SCH = ZDBCRC_SCH;
 constexpr int WG_PER_CU = 2;              // 2 x 70 KiB of LDS tables per CU
-constexpr uint64_t UNIT_OVH = 16;         // planning charge per record, in pieces
+// planning charge per record, in pieces: what a record boundary costs a wave
+// (segment reduction, pad shift, metadata, a partly used superstep) measured
+// in streaming time -- 384 balances C3 best (16: 0.811 ms, 256: 0.769,
+// 384: 0.765, 512: 0.779; profiles/r1/ab_unit_ovh.jsonl)
+constexpr uint32_t UNIT_OVH = 384;
 constexpr uint64_t MIN_UNITS_PER_WAVE = 256;
 
 static_assert(ZDBCRC_LDS_DW % 4 == 0, "LDS image must be 16-byte granular");
@@ -280,6 +284,7 @@ __device__ __forceinline__ void load_meta(MetaBatch &m, uint64_t rb, uint64_t n,
     }
 }
 
+template <uint32_t UO>
 __device__ __forceinline__ bool next_seg_batched(uint64_t &r, uint64_t n, uint64_t ub, uint64_t ue, uint32_t lane,
                                                  MetaBatch &m, const uint64_t *__restrict__ unit_start,
                                                  const uint8_t *arena, const uint64_t *__restrict__ offsets,
@@ -293,7 +298,7 @@ __device__ __forceinline__ bool next_seg_batched(uint64_t &r, uint64_t n, uint64
         const uint64_t u0 = readlane64(m.u0, li);
         if (u0 >= ue)
             return false;
-        const uint64_t us = u0 + UNIT_OVH;
+        const uint64_t us = u0 + UO;
         const uint64_t ur = readlane64(m.ur, li);
         const uint64_t s_lo = ub > us ? ub : us;
         const uint64_t s_hi = ue < ur ? ue : ur;
@@ -334,10 +339,11 @@ __device__ __forceinline__ void load_superstep_v3(const SegCtx &s, uint32_t ss, 
     }
 }
 
+template <bool NOZ = false>
 __device__ __forceinline__ uint32_t seg_value_v3(const Seg &sg, uint32_t acc, uint32_t lane, const uint32_t *lds,
                                                  const uint32_t *__restrict__ tables) {
     uint32_t x = wave_xor_scalar(lane_place(acc, lane, lds));
-    if (sg.z)
+    if (!NOZ && sg.z)
         x = uniform_shift(x, tables + ZDBCRC_OFF_Z + sg.z * SCH * 32);
     // shift over the record pieces after the segment: one round per nonzero
     // radix-256 digit (at most 4 dependent table reads, usually 0-2)
@@ -354,14 +360,17 @@ __device__ __forceinline__ uint32_t seg_value_v3(const Seg &sg, uint32_t acc, ui
 // superstep and the slower half raises its issue priority (s_setprio 3).
 // Without it the co-resident waves of a CU finish up to 2x apart (age-ordered
 // arbitration; measured with the STAMP build) and the kernel ends on a tail.
-template <int WGT, int WPE, bool STAMP = false, int PRIO = 0>
+// NOZ: timing diagnostic only (skips the trailing-pad shift: wrong checksums)
+template <int WGT, int WPE, bool STAMP = false, int PRIO = 0, uint32_t UO = UNIT_OVH, bool NOZ = false>
 __global__ __launch_bounds__(WGT, WPE) void crc_batch_kernel_v3(
     const uint8_t *__restrict__ arena, const uint64_t *__restrict__ offsets,
     const uint32_t *__restrict__ lengths, const uint64_t *__restrict__ unit_start, uint64_t n,
     uint32_t *__restrict__ out, const uint32_t *__restrict__ tables, uint32_t max_waves,
     uint32_t *__restrict__ scratch, uint32_t epoch) {
-    __shared__ __attribute__((aligned(16))) uint32_t lds[ZDBCRC_LDS_DW + 16];
-    uint32_t *const prog = lds + ZDBCRC_LDS_DW; // per-wave progress (PRIO)
+    constexpr uint32_t NW = WGT / 64, NSLOT = 2 * NW;
+    __shared__ __attribute__((aligned(16))) uint32_t lds[ZDBCRC_LDS_DW + 16 + 2 * NSLOT];
+    uint32_t *const prog = lds + ZDBCRC_LDS_DW;   // per-wave progress (PRIO)
+    uint32_t *const slot = prog + 16;             // cut records of the workgroup: [NSLOT] r, [NSLOT] x
     const uint64_t t_start = STAMP ? __builtin_amdgcn_s_memrealtime() : 0;
 
     // locate this wave's slice and issue its first loads before the table
@@ -383,13 +392,15 @@ __global__ __launch_bounds__(WGT, WPE) void crc_batch_kernel_v3(
     if (active) {
         rn = find_record(unit_start, n, ub, lane);
         load_meta(m, rn, n, lane, unit_start, arena, offsets, lengths);
-        active = next_seg_batched(rn, n, ub, ue, lane, m, unit_start, arena, offsets, lengths, cur);
+        active = next_seg_batched<UO>(rn, n, ub, ue, lane, m, unit_start, arena, offsets, lengths, cur);
         if (active)
             load_superstep_v3(cur.c, 0, lane, bufc);
     }
     const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     if (PRIO && lane == 0)
         prog[wid] = active ? 0u : 0xFFFFFFFFu; // an idle wave counts as ahead of everyone
+    if (lane < 2)
+        slot[2 * wid + lane] = ~0u;
     {
         const uint4 *src = reinterpret_cast<const uint4 *>(tables);
         uint4 *dst = reinterpret_cast<uint4 *>(lds);
@@ -421,7 +432,7 @@ __global__ __launch_bounds__(WGT, WPE) void crc_batch_kernel_v3(
         if (css + 1 < cur.S) {
             nx = cur;
             nss = css + 1;
-        } else if (!next_seg_batched(rn, n, ub, ue, lane, m, unit_start, arena, offsets, lengths, nx)) {
+        } else if (!next_seg_batched<UO>(rn, n, ub, ue, lane, m, unit_start, arena, offsets, lengths, nx)) {
             more = false;
             nx = cur;
             nss = css;
@@ -434,7 +445,7 @@ __global__ __launch_bounds__(WGT, WPE) void crc_batch_kernel_v3(
         uint32_t *dst = dummy;
         uint32_t x = 0;
         if (css + 1 == cur.S) {
-            x = seg_value_v3(cur, acc, lane, lds, tables);
+            x = seg_value_v3<NOZ>(cur, acc, lane, lds, tables);
             acc = 0;
             if (cur.c.pa == 0 && cur.pb == cur.c.np) {
                 dst = out + cur.r;
@@ -463,9 +474,29 @@ __global__ __launch_bounds__(WGT, WPE) void crc_batch_kernel_v3(
         st[2] = __builtin_amdgcn_s_getreg(0xF804); // HW_REG_HW_ID: wave/simd/cu/se
         st[3] = __builtin_amdgcn_s_getreg(0xF814); // HW_REG_XCC_ID
     }
-    if (lane == 0) {
-        for (uint32_t i = 0; i < ncut && i < 2; i++)
-            atomicXor(out + cut_r[i], cut_x[i]);
+    // records cut by a slice edge: combine the workgroup's partial values in
+    // LDS first (consecutive waves cut the same record; a record spanning many
+    // slices would otherwise take one same-address atomic per wave), then one
+    // atomic XOR per distinct record.  Waves that left early are not counted
+    // by the barrier; their slots hold ~0.
+    if (lane < 2 && lane < ncut) {
+        slot[2 * wid + lane] = (uint32_t)cut_r[lane];
+        slot[NSLOT + 2 * wid + lane] = cut_x[lane];
+    }
+    __syncthreads();
+    const uint32_t r_l = lane < NSLOT ? slot[lane] : ~0u;
+    const uint32_t x_l = lane < NSLOT ? slot[NSLOT + lane] : 0u;
+#pragma unroll
+    for (uint32_t i = 0; i < 2; i++) {
+        const uint32_t s_i = 2 * wid + i;
+        const uint32_t r_s = __builtin_amdgcn_readlane(r_l, s_i);
+        if (r_s == ~0u)
+            continue;
+        if (__ballot(lane < s_i && r_l == r_s) != 0)
+            continue; // a lower slot owns this record
+        const uint32_t v = wave_xor_scalar(r_l == r_s ? x_l : 0u);
+        if (lane == 0)
+            atomicXor(out + r_s, v);
     }
 }
 
@@ -477,6 +508,7 @@ struct KernelVariant {
     crc_kernel_fn fn;
     int threads;
     int wgs_per_cu = WG_PER_CU;
+    uint32_t unit_ovh = UNIT_OVH; // must match the kernel's UO
 };
 
 // selectable with ZDBCRC_VARIANT=<index> (A/B measurement); 0 is the default
@@ -485,6 +517,8 @@ const KernelVariant kVariants[] = {
     {"v3_wg768", crc_batch_kernel_v3<768, 6>, 768},
     {"v3_wg768_prio_stamp", crc_batch_kernel_v3<768, 6, true, 1>, 768},
     {"v3_wg768_stamp", crc_batch_kernel_v3<768, 6, true>, 768},
+    {"v3_wg768_prio_ovh16", crc_batch_kernel_v3<768, 6, false, 1, 16>, 768, WG_PER_CU, 16},
+    {"v3_wg768_prio_noz", crc_batch_kernel_v3<768, 6, false, 1, UNIT_OVH, true>, 768},
 };
 
 constexpr int kNumVariants = (int)(sizeof(kVariants) / sizeof(kVariants[0]));
@@ -499,20 +533,22 @@ const KernelVariant &variant() {
     return kVariants[g_variant];
 }
 
-// unit count per record: UNIT_OVH + number of 16-byte pieces it touches
+// unit count per record: ovh (the variant's per-record charge) + number of
+// 16-byte pieces it touches
 struct UnitCount {
     const uint8_t *arena;
     const uint64_t *offsets;
     const uint32_t *lengths;
     uint64_t n;
+    uint64_t ovh;
     __host__ __device__ uint64_t operator()(uint64_t r) const {
         if (r >= n)
             return 0;
         const uint32_t L = lengths[r];
         if (!L)
-            return UNIT_OVH;
+            return ovh;
         const uint64_t a = reinterpret_cast<uint64_t>(arena) + offsets[r];
-        return UNIT_OVH + (((a + L - 1) >> 4) - (a >> 4) + 1);
+        return ovh + (((a + L - 1) >> 4) - (a >> 4) + 1);
     }
 };
 
@@ -672,7 +708,7 @@ int ensure_device(DeviceCtx **out_ctx, int *out_dev) {
 size_t scan_temp_bytes(uint64_t n) {
     size_t bytes = 0;
     auto it = rocprim::make_transform_iterator(rocprim::counting_iterator<uint64_t>(0),
-                                               UnitCount{nullptr, nullptr, nullptr, n});
+                                               UnitCount{nullptr, nullptr, nullptr, n, UNIT_OVH});
     rocprim::exclusive_scan(nullptr, bytes, it, static_cast<uint64_t *>(nullptr), uint64_t(0),
                             n + 1, rocprim::plus<uint64_t>());
     return bytes;
@@ -717,7 +753,7 @@ int enqueue_batch(DeviceCtx &c, const uint8_t *arena, const uint64_t *offsets, c
         void *tmp = static_cast<uint8_t *>(w.ptr) + scratch_bytes + us_bytes;
         size_t tb = tmp_bytes;
         auto it = rocprim::make_transform_iterator(rocprim::counting_iterator<uint64_t>(0),
-                                                   UnitCount{arena, offsets, lengths, n});
+                                                   UnitCount{arena, offsets, lengths, n, variant().unit_ovh});
         if (rocprim::exclusive_scan(tmp, tb, it, us, uint64_t(0), n + 1, rocprim::plus<uint64_t>(), st) !=
             hipSuccess)
             return ZDB_CRC32_ELAUNCH;
@@ -929,7 +965,7 @@ int zdb_crc32_batch(const uint8_t *arena, size_t arena_len, const uint64_t *offs
     uint32_t *hout = reinterpret_cast<uint32_t *>(h.hplan + n * 12 + (n + 1) * 8);
     std::memcpy(ho, offsets, n * 8);
     std::memcpy(hl, lengths, n * 4);
-    const UnitCount uc{h.arena, offsets, lengths, n};
+    const UnitCount uc{h.arena, offsets, lengths, n, variant().unit_ovh};
     uint64_t acc = 0;
     for (size_t r = 0; r < n; r++) {
         hu[r] = acc;

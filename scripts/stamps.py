@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Per-wave start/end spread of the checksum kernel (diagnostic STAMP variant):
 is the kernel's end set by a tail of slow waves?"""
-import ctypes as C, json, sys
+import ctypes as C, json, sys, time
 from pathlib import Path
 import numpy as np
 ROOT = Path(__file__).resolve().parents[1]
@@ -12,21 +12,35 @@ rd = zdbcrc._lib.zdbcrc_debug_read_stamps; rd.restype = C.c_int; rd.argtypes = [
 vname = sys.argv[2] if len(sys.argv) > 2 else "v3_wg768_stamp"
 idx = [i for i in range(20) if sv(i) and sv(i).decode() == vname][0]
 sv(idx)
-for wl in sys.argv[1].split(","):
+for label in sys.argv[1].split(","):
+    wl, size = label, 4 << 30
+    if "@" in wl:
+        wl, mib = wl.split("@")
+        size = int(mib) << 20
     if wl == "zipf":
-        lens = zdbcrc.zipf_lengths(4 << 30, 0xC3C3C3).astype(np.int64)
+        lens = zdbcrc.zipf_lengths(size, 0xC3C3C3).astype(np.int64)
     elif wl == "fixed4k":
-        lens = np.full(1 << 20, 4096, np.int64)
+        lens = np.full(size >> 12, 4096, np.int64)
     else:
-        lens = np.array([(4 << 30) - 16], np.int64)
+        lens = np.array([size - 16], np.int64)
     offs = np.zeros(len(lens), np.int64); offs[1:] = np.cumsum(lens[:-1])
     arena = torch.empty(int(offs[-1] + lens[-1]) + 64, dtype=torch.uint8, device="cuda")
     zdbcrc.synth_fill_device(arena, 1)
     do, dl = torch.from_numpy(offs).cuda(), torch.from_numpy(lens.astype(np.int32)).cuda()
     out = torch.empty(len(lens), dtype=torch.int32, device="cuda")
-    for _ in range(4):
+    t_end = time.time() + 1.0  # ~1 s of back-to-back work first: clocks settle
+    while time.time() < t_end:
+        for _ in range(8):
+            zdbcrc.batch_device(arena, do, dl, out)
+        torch.cuda.synchronize()
+    # back-to-back launches (steady clocks); the stamps are the last launch's
+    zdbcrc.kernel_stats(); zdbcrc.set_timing(True)
+    for _ in range(8):
         zdbcrc.batch_device(arena, do, dl, out)
-    torch.cuda.synchronize()
+    torch.cuda.synchronize(); zdbcrc.set_timing(False)
+    kms, nl = zdbcrc.kernel_stats()
+    kms /= nl
+    print(json.dumps({"workload": label, "variant": vname, "kernel_ms_event": round(kms, 4)}))
     waves = 256 * 2 * 12
     st = np.zeros(waves * 4, np.uint64)
     assert rd(st.ctypes.data, waves) == 0
@@ -64,7 +78,10 @@ for wl in sys.argv[1].split(","):
                       "cu_mean_end_us_min_p50_max": [round(float(x), 1) for x in (cu_mean.min(), np.median(cu_mean), cu_mean.max())],
                       "within_cu_spread_us_p50_max": [round(float(np.median(cu_spread)), 1), round(float(cu_spread.max()), 1)],
                       "xcd_mean_end_us": per_x}))
-    print(json.dumps({"workload": wl, "waves": len(st), "start_us_p50_max": [round(float(np.median(s_)), 1), round(float(s_.max()), 1)],
+    print(json.dumps({"workload": label, "waves": len(st), "start_us_p50_max": [round(float(np.median(s_)), 1), round(float(s_.max()), 1)],
                       "end_us_p10_p50_p90_max": [round(float(np.percentile(e_, q)), 1) for q in (10, 50, 90, 100)],
                       "dur_us_min_p50_max": [round(float(dur.min()), 1), round(float(np.median(dur)), 1), round(float(dur.max()), 1)]}))
     del arena
+    slow = np.argsort(dur)[-8:][::-1]
+    print(json.dumps({"workload": label, "slowest_waves": [[int(gw[i]), round(float(s_[i]), 1), round(float(dur[i]), 1)]
+                                                             for i in slow]}))

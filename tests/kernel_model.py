@@ -19,7 +19,7 @@ OFF_Z = LDS_DW
 OFF_R = OFF_Z + 16 * SCH * 32
 RDIG = 4
 TABLE_DW = OFF_R + RDIG * 256 * SCH * 32
-UNIT_OVH = 16
+UNIT_OVH = 384
 MIN_UNITS_PER_WAVE = 256
 
 LANES = np.arange(WAVE, dtype=np.int64)
