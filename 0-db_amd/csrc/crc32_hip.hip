@@ -1008,8 +1008,8 @@ void zdb_crc32_set_timing(int enable) {
     g_timing = enable != 0;
 }
 
-int zdb_crc32_kernel_stats(double *total_ms, uint64_t *launches) {
-    std::lock_guard<std::mutex> g(g_mu);
+static int drain_timing(float *each, size_t max_each, size_t *n_each) {
+    size_t k = 0;
     for (auto &p : g_pending) {
         if (hipEventSynchronize(p.second) != hipSuccess)
             return ZDB_CRC32_ELAUNCH;
@@ -1017,10 +1017,32 @@ int zdb_crc32_kernel_stats(double *total_ms, uint64_t *launches) {
         hipEventElapsedTime(&ms, p.first, p.second);
         g_time_ms += ms;
         g_launches += 1;
+        if (each && k < max_each)
+            each[k++] = ms;
         g_event_pool.push_back(p.first);
         g_event_pool.push_back(p.second);
     }
     g_pending.clear();
+    if (n_each)
+        *n_each = k;
+    return ZDB_CRC32_OK;
+}
+
+// debug: per-launch kernel times (ms) recorded since the last drain
+long zdbcrc_debug_kernel_times(float *each, size_t max_each) {
+    std::lock_guard<std::mutex> g(g_mu);
+    size_t k = 0;
+    if (drain_timing(each, max_each, &k))
+        return -1;
+    g_time_ms = 0;
+    g_launches = 0;
+    return (long)k;
+}
+
+int zdb_crc32_kernel_stats(double *total_ms, uint64_t *launches) {
+    std::lock_guard<std::mutex> g(g_mu);
+    if (int rc = drain_timing(nullptr, 0, nullptr))
+        return rc;
     if (total_ms)
         *total_ms = g_time_ms;
     if (launches)

@@ -8,5 +8,6 @@ timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_ou
 timeout -k 10 600 python -m pytest tests -q -m gpu > gpurun_out/$T/pytest_gpu.log 2>&1 && \
 timeout -k 10 400 python bench.py > gpurun_out/$T/bench.json 2> gpurun_out/$T/bench.err && \
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/$T/trace -o run -- \
-    python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-extra > gpurun_out/$T/trace_bench.json 2> gpurun_out/$T/trace_bench.err && \
+    python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-extra > gpurun_out/$T/trace_bench.json 2> gpurun_out/$T/trace_bench.err && \
+python3 scripts/trace_summary.py gpurun_out/$T/trace/run_kernel_trace.csv 20 > gpurun_out/$T/trace_summary.json && \
 TAG=$T/pmc PMC_FILE=scripts/pmc_v3.txt bash scripts/profile_pmc.sh
