@@ -42,9 +42,6 @@
 #include <vector>
 
 #include <hip/hip_runtime.h>
-#include <rocprim/device/device_scan.hpp>
-#include <rocprim/iterator/counting_iterator.hpp>
-#include <rocprim/iterator/transform_iterator.hpp>
 
 #include "crc32c_gf2.h"
 #include "zdb_crc32.h"
@@ -239,15 +236,38 @@ __device__ __forceinline__ uint32_t wave_xor_scalar(uint32_t x) {
            __builtin_amdgcn_readlane(x, 32) ^ __builtin_amdgcn_readlane(x, 48);
 }
 
+// per-record unit prefix as the planner leaves it: local[r] is the prefix
+// inside r's block of 2^lg records and boff[b] (built in LDS by every
+// workgroup from the planner's block totals) the prefix of whole blocks:
+// unit_start(r) = local[r] + boff[r >> lg].  boff == nullptr when local
+// already holds the global prefix (host-planned batches).
+constexpr uint32_t PLAN_MAX_BLOCKS = 1024; // block offsets kept in LDS
+struct UnitPrefix {
+    const uint64_t *local;
+    const uint64_t *boff;
+    uint32_t lg;
+    __device__ __forceinline__ uint64_t operator()(uint64_t r) const {
+        return boff ? local[r] + boff[r >> lg] : local[r];
+    }
+};
+
+// what the planner hands the checksum kernel
+struct PlanArgs {
+    const uint64_t *local; // n + 1 entries
+    const uint64_t *bsum;  // nb block totals (nullptr: local is global)
+    uint32_t nb;
+    uint32_t lg;
+};
+
 // record r with unit_start[r] <= b < unit_start[r+1]: 64-way search, one
 // vector load per round (3 rounds for 1e5 records, 4 for 1e6)
-__device__ __forceinline__ uint64_t find_record(const uint64_t *__restrict__ unit_start, uint64_t n, uint64_t b,
+__device__ __forceinline__ uint64_t find_record(const UnitPrefix &unit_start, uint64_t n, uint64_t b,
                                                 uint32_t lane) {
     uint64_t lo = 0, hi = n;
     while (hi - lo > 1) {
         const uint64_t step = (hi - lo + 63) >> 6;
         const uint64_t idx = lo + (uint64_t)lane * step;
-        const bool le = idx < hi && unit_start[idx] <= b;
+        const bool le = idx < hi && unit_start(idx) <= b;
         const uint64_t mask = __ballot(le);
         const uint32_t L = 63u - (uint32_t)__clzll(mask);
         lo += (uint64_t)L * step;
@@ -267,7 +287,7 @@ struct MetaBatch {
 };
 
 __device__ __forceinline__ void load_meta(MetaBatch &m, uint64_t rb, uint64_t n, uint32_t lane,
-                                          const uint64_t *__restrict__ unit_start, const uint8_t *arena,
+                                          const UnitPrefix &unit_start, const uint8_t *arena,
                                           const uint64_t *__restrict__ offsets,
                                           const uint32_t *__restrict__ lengths) {
     m.rb = rb;
@@ -277,8 +297,8 @@ __device__ __forceinline__ void load_meta(MetaBatch &m, uint64_t rb, uint64_t n,
     m.addr = 0;
     m.len = 0;
     if (r < n) {
-        m.u0 = unit_start[r];
-        m.ur = unit_start[r + 1];
+        m.u0 = unit_start(r);
+        m.ur = unit_start(r + 1);
         m.addr = reinterpret_cast<uint64_t>(arena) + offsets[r];
         m.len = lengths[r];
     }
@@ -286,7 +306,7 @@ __device__ __forceinline__ void load_meta(MetaBatch &m, uint64_t rb, uint64_t n,
 
 template <uint32_t UO>
 __device__ __forceinline__ bool next_seg_batched(uint64_t &r, uint64_t n, uint64_t ub, uint64_t ue, uint32_t lane,
-                                                 MetaBatch &m, const uint64_t *__restrict__ unit_start,
+                                                 MetaBatch &m, const UnitPrefix &unit_start,
                                                  const uint8_t *arena, const uint64_t *__restrict__ offsets,
                                                  const uint32_t *__restrict__ lengths, Seg &sg) {
     for (;;) {
@@ -354,6 +374,41 @@ __device__ __forceinline__ uint32_t seg_value_v3(const Seg &sg, uint32_t acc, ui
     return x;
 }
 
+__device__ __forceinline__ uint64_t wave_incl_scan64(uint64_t v, uint32_t lane) {
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint64_t t = __shfl_up(v, o, 64);
+        if (lane >= (uint32_t)o)
+            v += t;
+    }
+    return v;
+}
+
+// exclusive scan of one value per thread across an NT-thread block;
+// *total = the sum; wsum: 2 (NT / 64) + 1 entries of LDS
+template <uint32_t NT>
+__device__ __forceinline__ uint64_t block_excl_scan64(uint64_t v, uint64_t *wsum, uint64_t *total) {
+    constexpr uint32_t NW = NT / 64;
+    const uint32_t lane = threadIdx.x & 63u, wid = threadIdx.x >> 6;
+    const uint64_t incl = wave_incl_scan64(v, lane);
+    if (lane == 63)
+        wsum[wid] = incl;
+    __syncthreads();
+    if (wid == 0) {
+        const uint64_t w = lane < NW ? wsum[lane] : 0;
+        const uint64_t wi = wave_incl_scan64(w, lane);
+        if (lane < NW)
+            wsum[NW + lane] = wi - w;
+        if (lane == NW - 1)
+            wsum[2 * NW] = wi;
+    }
+    __syncthreads();
+    *total = wsum[2 * NW];
+    const uint64_t r = incl - v + wsum[NW + wid];
+    __syncthreads(); // wsum reusable
+    return r;
+}
+
 // STAMP (diagnostic build only): each wave writes its start/end
 // s_memrealtime to scratch[16384 + 4 gw ...] -- never read by the kernel
 // PRIO: waves of a workgroup publish their progress in LDS every other
@@ -364,21 +419,47 @@ __device__ __forceinline__ uint32_t seg_value_v3(const Seg &sg, uint32_t acc, ui
 template <int WGT, int WPE, bool STAMP = false, int PRIO = 0, uint32_t UO = UNIT_OVH, bool NOZ = false>
 __global__ __launch_bounds__(WGT, WPE) void crc_batch_kernel_v3(
     const uint8_t *__restrict__ arena, const uint64_t *__restrict__ offsets,
-    const uint32_t *__restrict__ lengths, const uint64_t *__restrict__ unit_start, uint64_t n,
+    const uint32_t *__restrict__ lengths, const PlanArgs plan, uint64_t n,
     uint32_t *__restrict__ out, const uint32_t *__restrict__ tables, uint32_t max_waves,
     uint32_t *__restrict__ scratch, uint32_t epoch) {
     constexpr uint32_t NW = WGT / 64, NSLOT = 2 * NW;
     __shared__ __attribute__((aligned(16))) uint32_t lds[ZDBCRC_LDS_DW + 16 + 2 * NSLOT];
+    __shared__ uint64_t boff[PLAN_MAX_BLOCKS + 1];
+    __shared__ uint64_t wsum[2 * NW + 1];
     uint32_t *const prog = lds + ZDBCRC_LDS_DW;   // per-wave progress (PRIO)
     uint32_t *const slot = prog + 16;             // cut records of the workgroup: [NSLOT] r, [NSLOT] x
     const uint64_t t_start = STAMP ? __builtin_amdgcn_s_memrealtime() : 0;
+
+    // block offsets of the unit prefix (planner block totals, scanned here)
+    UnitPrefix unit_start{plan.local, nullptr, plan.lg};
+    if (plan.bsum) {
+        constexpr uint32_t PER = (PLAN_MAX_BLOCKS + WGT - 1) / WGT;
+        uint64_t v[PER], t = 0;
+#pragma unroll
+        for (uint32_t i = 0; i < PER; i++) {
+            const uint32_t b = threadIdx.x * PER + i;
+            v[i] = b < plan.nb ? plan.bsum[b] : 0;
+            t += v[i];
+        }
+        uint64_t total;
+        uint64_t e = block_excl_scan64<WGT>(t, wsum, &total);
+#pragma unroll
+        for (uint32_t i = 0; i < PER; i++) {
+            const uint32_t b = threadIdx.x * PER + i;
+            if (b <= plan.nb)
+                boff[b] = e;
+            e += v[i];
+        }
+        __syncthreads();
+        unit_start.boff = boff;
+    }
 
     // locate this wave's slice and issue its first loads before the table
     // fill, so the first HBM round trip overlaps the LDS copy; every wave
     // reaches the barrier below, active or not
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t gw = __builtin_amdgcn_readfirstlane(blockIdx.x * (WGT / 64) + (threadIdx.x >> 6));
-    const uint64_t total = unit_start[n];
+    const uint64_t total = unit_start(n);
     uint64_t nwaves = (total + MIN_UNITS_PER_WAVE - 1) / MIN_UNITS_PER_WAVE;
     if (nwaves > max_waves)
         nwaves = max_waves;
@@ -500,7 +581,7 @@ __global__ __launch_bounds__(WGT, WPE) void crc_batch_kernel_v3(
     }
 }
 
-typedef void (*crc_kernel_fn)(const uint8_t *, const uint64_t *, const uint32_t *, const uint64_t *, uint64_t,
+typedef void (*crc_kernel_fn)(const uint8_t *, const uint64_t *, const uint32_t *, PlanArgs, uint64_t,
                               uint32_t *, const uint32_t *, uint32_t, uint32_t *, uint32_t);
 
 struct KernelVariant {
@@ -551,6 +632,56 @@ struct UnitCount {
         return ovh + (((a + L - 1) >> 4) - (a >> 4) + 1);
     }
 };
+
+// planner (one launch): every record's unit count, the exclusive prefix
+// inside blocks of 2^lg records (local: n + 1 entries, entry n closes the
+// last block) and each block's total (bsum); zeroes out[] on the way (cut
+// records are finished by atomic XOR).  The checksum kernel scans the <= 1024
+// block totals itself, so there is no grid-wide dependency here.
+constexpr uint32_t PLAN_T = 256;
+
+__global__ __launch_bounds__(PLAN_T) void plan_kernel(const uint8_t *__restrict__ arena,
+                                                      const uint64_t *__restrict__ offsets,
+                                                      const uint32_t *__restrict__ lengths, uint64_t n, uint64_t ovh,
+                                                      uint32_t lg, uint64_t *__restrict__ local,
+                                                      uint64_t *__restrict__ bsum, uint32_t *__restrict__ out) {
+    __shared__ uint64_t wsum[2 * (PLAN_T / 64) + 1];
+    const uint32_t per = (1u << lg) / PLAN_T;
+    const uint64_t r0 = ((uint64_t)blockIdx.x << lg) + (uint64_t)threadIdx.x * per;
+    uint64_t s = 0;
+    for (uint32_t i = 0; i < per; i++) {
+        const uint64_t r = r0 + i;
+        if (r < n) {
+            const uint32_t L = lengths[r];
+            uint64_t v = ovh;
+            if (L) {
+                const uint64_t a = reinterpret_cast<uint64_t>(arena) + offsets[r];
+                v += ((a + L - 1) >> 4) - (a >> 4) + 1;
+            }
+            s += v;
+            out[r] = 0;
+        }
+    }
+    uint64_t total;
+    uint64_t e = block_excl_scan64<PLAN_T>(s, wsum, &total);
+    for (uint32_t i = 0; i < per; i++) {
+        const uint64_t r = r0 + i;
+        if (r > n)
+            break;
+        local[r] = e;
+        if (r < n) {
+            const uint32_t L = lengths[r];
+            uint64_t v = ovh;
+            if (L) {
+                const uint64_t a = reinterpret_cast<uint64_t>(arena) + offsets[r];
+                v += ((a + L - 1) >> 4) - (a >> 4) + 1;
+            }
+            e += v;
+        }
+    }
+    if (threadIdx.x == 0)
+        bsum[blockIdx.x] = total;
+}
 
 __global__ void verify_kernel(const uint32_t *__restrict__ out, const uint32_t *__restrict__ expected,
                               uint64_t n, uint32_t *__restrict__ mismatch, uint32_t *__restrict__ count,
@@ -705,14 +836,6 @@ int ensure_device(DeviceCtx **out_ctx, int *out_dev) {
     return ZDB_CRC32_OK;
 }
 
-size_t scan_temp_bytes(uint64_t n) {
-    size_t bytes = 0;
-    auto it = rocprim::make_transform_iterator(rocprim::counting_iterator<uint64_t>(0),
-                                               UnitCount{nullptr, nullptr, nullptr, n, UNIT_OVH});
-    rocprim::exclusive_scan(nullptr, bytes, it, static_cast<uint64_t *>(nullptr), uint64_t(0),
-                            n + 1, rocprim::plus<uint64_t>());
-    return bytes;
-}
 
 // enqueue memset + plan scan + main kernel; caller holds g_mu
 // d_unit_start: the per-record unit prefix when the caller already has it
@@ -721,14 +844,18 @@ int enqueue_batch(DeviceCtx &c, const uint8_t *arena, const uint64_t *offsets, c
                   uint32_t *out, uint64_t n, hipStream_t st, const uint64_t *d_unit_start = nullptr) {
     if (n > 0xFFFFFFFFull) // record indices are 32-bit on the device (cut lists, mismatch indices)
         return ZDB_CRC32_EINVAL;
-    if (hipMemsetAsync(out, 0, n * sizeof(uint32_t), st) != hipSuccess)
-        return ZDB_CRC32_ELAUNCH;
-
-    const size_t us_bytes = d_unit_start ? 0 : ((n + 1) * sizeof(uint64_t) + 255) & ~size_t(255);
-    const size_t tmp_bytes = d_unit_start ? 0 : scan_temp_bytes(n);
-    // dummy dword per wave (64 KiB) | diagnostic stamps (448 KiB) | chunk counters (v4)
+    const KernelVariant &kv = variant();
+    // planner blocks: 2^lg records each (n + 1 entries), at most PLAN_MAX_BLOCKS
+    uint32_t lg = 10;
+    while (((n + 1 + (1ull << lg) - 1) >> lg) > PLAN_MAX_BLOCKS)
+        lg++;
+    const uint64_t nb = (n + 1 + (1ull << lg) - 1) >> lg;
+    auto al = [](size_t x) { return (x + 255) & ~size_t(255); };
+    const size_t local_bytes = d_unit_start ? 0 : al((n + 1) * sizeof(uint64_t));
+    const size_t bsum_bytes = d_unit_start ? 0 : al(nb * sizeof(uint64_t));
+    // dummy dword per wave (64 KiB) | diagnostic stamps (448 KiB) | spare
     const size_t scratch_bytes = (64 + 448 + 4) * 1024;
-    const size_t need = us_bytes + scratch_bytes + tmp_bytes + 256;
+    const size_t need = scratch_bytes + local_bytes + bsum_bytes;
     Workspace &w = c.ws[reinterpret_cast<void *>(st)];
     if (w.bytes < need) {
         if (w.ptr) {
@@ -740,27 +867,26 @@ int enqueue_batch(DeviceCtx &c, const uint8_t *arena, const uint64_t *offsets, c
         if (hipMalloc(&w.ptr, need) != hipSuccess)
             return ZDB_CRC32_ENOMEM;
         w.bytes = need;
-        // the v4 chunk counters start at 0; each launch leaves them at 0
         if (hipMemsetAsync(w.ptr, 0, need, st) != hipSuccess)
             return ZDB_CRC32_ELAUNCH;
     }
-    // scratch first: its offset (and the v4 counters in it) must not move with n
-    const uint64_t *unit_start = d_unit_start;
+    // scratch first: its offset must not move with n
     uint32_t *scratch = static_cast<uint32_t *>(w.ptr);
     g_last_scratch = scratch;
+    PlanArgs plan{d_unit_start, nullptr, 0, 0};
     if (!d_unit_start) {
-        uint64_t *us = reinterpret_cast<uint64_t *>(static_cast<uint8_t *>(w.ptr) + scratch_bytes);
-        void *tmp = static_cast<uint8_t *>(w.ptr) + scratch_bytes + us_bytes;
-        size_t tb = tmp_bytes;
-        auto it = rocprim::make_transform_iterator(rocprim::counting_iterator<uint64_t>(0),
-                                                   UnitCount{arena, offsets, lengths, n, variant().unit_ovh});
-        if (rocprim::exclusive_scan(tmp, tb, it, us, uint64_t(0), n + 1, rocprim::plus<uint64_t>(), st) !=
-            hipSuccess)
+        uint8_t *base = static_cast<uint8_t *>(w.ptr) + scratch_bytes;
+        uint64_t *local = reinterpret_cast<uint64_t *>(base);
+        uint64_t *bsum = reinterpret_cast<uint64_t *>(base + local_bytes);
+        hipLaunchKernelGGL(plan_kernel, dim3((uint32_t)nb), dim3(PLAN_T), 0, st, arena, offsets, lengths, n,
+                           (uint64_t)kv.unit_ovh, lg, local, bsum, out);
+        if (hipGetLastError() != hipSuccess)
             return ZDB_CRC32_ELAUNCH;
-        unit_start = us;
+        plan = PlanArgs{local, bsum, (uint32_t)nb, lg};
+    } else if (hipMemsetAsync(out, 0, n * sizeof(uint32_t), st) != hipSuccess) {
+        return ZDB_CRC32_ELAUNCH;
     }
 
-    const KernelVariant &kv = variant();
     const uint32_t grid = (uint32_t)(c.cus * kv.wgs_per_cu);
     const uint32_t max_waves = grid * (uint32_t)(kv.threads / 64);
     hipEvent_t e0 = nullptr, e1 = nullptr;
@@ -775,7 +901,7 @@ int enqueue_batch(DeviceCtx &c, const uint8_t *arena, const uint64_t *offsets, c
         }
         hipEventRecord(e0, st);
     }
-    hipLaunchKernelGGL(kv.fn, dim3(grid), dim3(kv.threads), 0, st, arena, offsets, lengths, unit_start, n,
+    hipLaunchKernelGGL(kv.fn, dim3(grid), dim3(kv.threads), 0, st, arena, offsets, lengths, plan, n,
                        out, c.d_tables, max_waves, scratch, ++c.epoch);
     if (hipGetLastError() != hipSuccess)
         return ZDB_CRC32_ELAUNCH;

@@ -10,7 +10,7 @@ path, steps = sys.argv[1], int(sys.argv[2])
 rows = defaultdict(list)
 for r in csv.DictReader(open(path)):
     name = r["Kernel_Name"]
-    short = ("crc_batch_kernel" if "crc_batch_kernel" in name else
+    short = ("crc_batch_kernel" if "crc_batch_kernel" in name else "plan_kernel" if "plan_kernel" in name else
              "rocprim_scan" if "trampoline_kernel" in name else
              "rocprim_scan_init" if "init_lookback" in name else name.split("(")[0][-48:])
     rows[short].append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]) - int(r["Start_Timestamp"])))
