@@ -27,6 +27,16 @@ if not LIB_PATH.exists():
         f"libzdbcrc.so not found at {LIB_PATH}: build it with `make -C 0-db_amd` "
         "(or __graft_entry__.build()); there is no fallback implementation")
 
+# torch's wheel carries its own HIP runtime (libamdhip64.so + its own HSA
+# runtime) beside the ROCm one this library links (libamdhip64.so.7).  The
+# two coexist in one process only when torch's is loaded first (the other
+# order leaves this library without a device), so load torch, when it is
+# installed, before the library.  Importing torch does not initialise a GPU.
+try:
+    import torch  # noqa: F401
+except ImportError:
+    pass
+
 _lib = C.CDLL(str(LIB_PATH))
 
 u8p = C.POINTER(C.c_uint8)

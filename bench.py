@@ -34,6 +34,14 @@ HBM_PEAK_GBS = 8000.0  # MI355X spec (MI355X_MICROARCH.md, chip-level parameters
 C2_SEED = 0x5A0DB5EED
 C3_SEED = 0x5A0DB5EED + 3
 C3_LEN_SEED = 0xC3C3C3
+C4_SEED = 0x5A0DB5EED + 4
+C4_LEN_SEED = 0xC4C4C4
+C4_FILES = 64
+C4_FILE_CAP = 256 << 20  # bytes per datafile (64 x 256 MiB per GPU)
+C4_KEY = 8               # key bytes per entry
+C4_TIMESTAMP = 1700000000
+ENTRY_HDR = 18           # data_entry_header_t (libzdb/data.h:56-65)
+FILE_HDR = 28            # data_header_t (libzdb/data.h:38-45)
 GIB = float(1 << 30)
 
 
@@ -56,9 +64,185 @@ def make_dataset(workload: str, target: int, rank: int):
         offs = np.arange(n, dtype=np.int64) * 4096
         seed = C2_SEED + rank
         desc = "C2: fixed 4 KiB records, 4 KiB-aligned"
+    elif workload == "c2u":
+        # the C2 payloads laid out as a datafile image (18 B
+        # entry header + 8 B key before each), so every payload is misaligned
+        n = target // 4096
+        lens = np.full(n, 4096, np.int64)
+        offs = FILE_HDR + np.arange(n, dtype=np.int64) * (ENTRY_HDR + C4_KEY + 4096) + ENTRY_HDR + C4_KEY
+        seed = C2_SEED + rank
+        desc = "C2u: fixed 4 KiB payloads inside a datafile image (26 B header+key each), misaligned"
     else:
         raise SystemExit(f"unknown workload {workload}")
     return offs, lens, seed, desc
+
+
+def c4_layout(rank: int, files: int = C4_FILES, file_cap: int = C4_FILE_CAP) -> dict:
+    """SURVEY §8(d) C4 shard of one GPU: reference-valid datafiles (format of
+    libzdb/data.h, version 3) holding C3-distributed payloads with 8-byte
+    keys, packed into `files` datafiles of at most `file_cap` bytes, placed
+    back to back in one arena.  Entry e's header sits at entry_off[e], its
+    key right after, its payload at payload_off[e]; `previous` is the
+    file-relative offset of the entry before it (0 for the first), as
+    data_insert writes it (data.c:594-633)."""
+    import zdbcrc
+    target = files * file_cap
+    lens = zdbcrc.zipf_lengths(target, C4_LEN_SEED + rank).astype(np.int64)
+    ent = ENTRY_HDR + C4_KEY + lens
+    file_of = np.zeros(len(lens), np.int64)
+    rel = np.zeros(len(lens), np.int64)  # file-relative entry offset
+    f, pos, n = 0, FILE_HDR, 0
+    for e in range(len(lens)):
+        if pos + ent[e] > file_cap:
+            f += 1
+            pos = FILE_HDR
+            if f == files:
+                break
+        file_of[e], rel[e] = f, pos
+        pos += ent[e]
+        n = e + 1
+    lens, ent, file_of, rel = lens[:n], ent[:n], file_of[:n], rel[:n]
+    nfiles = int(file_of[-1]) + 1
+    fsize = np.full(nfiles, FILE_HDR, np.int64)
+    np.add.at(fsize, file_of, ent)
+    file_off = np.zeros(nfiles, np.int64)
+    file_off[1:] = np.cumsum(fsize[:-1])
+    prev = np.zeros(n, np.int64)
+    same = np.zeros(n, bool)
+    same[1:] = file_of[1:] == file_of[:-1]
+    prev[1:][same[1:]] = rel[:-1][same[1:]]
+    entry_off = file_off[file_of] + rel
+    return {"lens": lens, "entry_off": entry_off, "payload_off": entry_off + ENTRY_HDR + C4_KEY,
+            "prev": prev, "file_of": file_of, "file_off": file_off, "file_size": fsize,
+            "total": int(file_off[-1] + fsize[-1])}
+
+
+def c4_entry_headers(layout: dict, crcs: np.ndarray) -> np.ndarray:
+    """(n, 26) bytes: data_entry_header_t (packed, little endian) + 8-byte key
+    (the entry index), with the payload crcs in `integrity`."""
+    n = len(layout["lens"])
+    dt = np.dtype([("idlength", "u1"), ("datalength", "<u4"), ("previous", "<u4"), ("integrity", "<u4"),
+                   ("flags", "u1"), ("timestamp", "<u4"), ("key", "<u8")])
+    assert dt.itemsize == ENTRY_HDR + C4_KEY
+    h = np.zeros(n, dt)
+    h["idlength"] = C4_KEY
+    h["datalength"] = layout["lens"]
+    h["previous"] = layout["prev"]
+    h["integrity"] = crcs
+    h["timestamp"] = C4_TIMESTAMP
+    h["key"] = np.arange(n, dtype=np.uint64)
+    return h.view(np.uint8).reshape(n, ENTRY_HDR + C4_KEY)
+
+
+def c4_file_headers(layout: dict) -> np.ndarray:
+    import zdbcrc
+    return np.stack([np.frombuffer(zdbcrc.encode_header(f), np.uint8)
+                     for f in range(len(layout["file_off"]))])
+
+
+def c4_image_host(layout: dict, seed: int, crcs: np.ndarray, files: int | None = None) -> np.ndarray:
+    """Host image of the first `files` datafiles of a C4 shard (tests, golden
+    checks): synthetic bytes at every arena position, then the headers."""
+    import zdbcrc
+    nf = len(layout["file_off"]) if files is None else files
+    end = int(layout["file_off"][nf - 1] + layout["file_size"][nf - 1])
+    img = zdbcrc.synth_fill(end, seed)
+    sel = layout["file_of"] < nf
+    hdr = c4_entry_headers(layout, crcs)[sel]
+    idx = layout["entry_off"][sel][:, None] + np.arange(ENTRY_HDR + C4_KEY)
+    img[idx] = hdr
+    fidx = layout["file_off"][:nf, None] + np.arange(FILE_HDR)
+    img[fidx] = c4_file_headers(layout)[:nf]
+    return img
+
+
+def c4_build_device(lay: dict, seed: int):
+    """The C4 images in HBM: synthetic bytes at every position, then the file
+    and entry headers (integrity = the payload crc from an untimed checksum
+    pass).  Returns (image, payload offsets, lengths, expected crcs read back
+    out of the image headers, host crcs)."""
+    import torch
+    import zdbcrc
+    n = len(lay["lens"])
+    img = torch.empty(lay["total"] + 64, dtype=torch.uint8, device="cuda")
+    zdbcrc.synth_fill_device(img, seed)
+    d_poff = torch.from_numpy(lay["payload_off"]).cuda()
+    d_len = torch.from_numpy(lay["lens"].astype(np.int32)).cuda()
+    out = torch.empty(n, dtype=torch.int32, device="cuda")
+    zdbcrc.batch_device(img, d_poff, d_len, out)
+    crcs = out.cpu().numpy().view(np.uint32).copy()
+    hdr = torch.from_numpy(c4_entry_headers(lay, crcs).reshape(-1)).cuda()
+    idx = torch.from_numpy((lay["entry_off"][:, None] + np.arange(ENTRY_HDR + C4_KEY)).reshape(-1)).cuda()
+    img[idx] = hdr
+    fidx = torch.from_numpy((lay["file_off"][:, None] + np.arange(FILE_HDR)).reshape(-1)).cuda()
+    img[fidx] = torch.from_numpy(c4_file_headers(lay).reshape(-1)).cuda()
+    del hdr, idx, fidx
+    ioff = torch.from_numpy(lay["entry_off"] + 9).cuda()  # `integrity` at byte 9 of the entry header
+    b = [img[ioff + i].to(torch.int64) for i in range(4)]
+    expected = (b[0] | (b[1] << 8) | (b[2] << 16) | (b[3] << 24)).to(torch.int32)
+    return img, d_poff, d_len, expected, crcs
+
+
+def c4_leg(rank: int, world: int, steps: int, warmup: int, settle_s: float, barrier) -> dict:
+    """the integrity scan of this rank's 64 reference-valid
+    datafiles (~16 GiB), device-resident: plan + checksum + compare with the
+    `integrity` field stored in each entry header (zdb_crc32_verify_device).
+    The image is built in HBM (synthetic bytes, then the headers, whose crcs
+    come from an untimed checksum pass and are checked against the golden
+    digest computed by the reference on the CPU)."""
+    import torch
+    import zdbcrc
+    lay = c4_layout(rank)
+    n = len(lay["lens"])
+    img, d_poff, d_len, expected, crcs = c4_build_device(lay, C4_SEED + rank)
+    out = torch.empty(n, dtype=torch.int32, device="cuda")
+    parity = "unchecked"
+    gold = ROOT / "tests" / "golden" / "digests.json"
+    if rank == 0 and gold.exists():
+        ref = json.loads(gold.read_text()).get("C4")
+        got = digest(crcs)
+        if ref:
+            ok = all(got[k] == ref[k] for k in ("count", "xor", "crc_of_crcs"))
+            parity = "bit-exact vs reference digest C4" if ok else f"MISMATCH {got} vs {ref}"
+    mism = torch.zeros(1024, dtype=torch.int32, device="cuda")
+    cnt = torch.zeros(1, dtype=torch.int32, device="cuda")
+
+    def step():
+        zdbcrc.verify_device(img, d_poff, d_len, expected, out, mism, cnt)
+
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize()
+    t_settle = time.perf_counter() + settle_s
+    while time.perf_counter() < t_settle:
+        step()
+        torch.cuda.synchronize()
+    barrier()
+    zdbcrc.kernel_stats()
+    zdbcrc.set_timing(True)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    barrier()
+    zdbcrc.set_timing(False)
+    km, kl = zdbcrc.kernel_stats()
+    mismatches = int(cnt.item())
+    payload = int(lay["lens"].sum())
+    elapsed, all_payload = combine_ranks(t1 - t0, payload, world)
+    kern_s = km / max(kl, 1) / 1e3
+    alg = payload + 20 * n  # integrity scan: + 4 B expected crc read (SURVEY §8(d))
+    res = {"desc": f"C4: integrity scan of {len(lay['file_off'])} reference-valid datafiles per GPU "
+                   f"({lay['total']} B images, {n} records, C3 payload sizes, 8 B keys), device-resident",
+           "records_per_gpu": n, "payload_bytes_per_gpu": payload, "n_gpus": world,
+           "gibs": round(all_payload * steps / elapsed / GIB, 2),
+           "ms_per_step": round(elapsed / steps * 1e3, 4), "kernel_ms": round(kern_s * 1e3, 4),
+           "roofline_frac": round(alg / kern_s / 1e9 / HBM_PEAK_GBS, 4),
+           "mismatches": mismatches, "parity": parity}
+    del img, out, expected
+    torch.cuda.empty_cache()
+    return res
 
 
 def digest(crcs: np.ndarray) -> dict:
@@ -232,11 +416,12 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--workload", default="zipf", choices=["zipf", "fixed4k"])
+    ap.add_argument("--workload", default="zipf", choices=["zipf", "fixed4k", "c2u"])
     ap.add_argument("--gib", type=float, default=4.0, help="batch size per GPU (GiB)")
     ap.add_argument("--cpu-seconds", type=float, default=3.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extra", action="store_true")
+    ap.add_argument("--no-c4", action="store_true", help="skip the C4 integrity-scan leg")
     ap.add_argument("--settle-s", type=float, default=1.0,
                     help="untimed steps after the warmup until this many seconds have passed")
     args = ap.parse_args()
@@ -279,8 +464,8 @@ def main():
     parity = "unchecked"
     gold = ROOT / "tests" / "golden" / "digests.json"
     if rank == 0 and gold.exists():
-        key = "C3" if args.workload == "zipf" else "C2"
-        ref = json.loads(gold.read_text()).get(key)
+        key = {"zipf": "C3", "fixed4k": "C2"}.get(args.workload)
+        ref = json.loads(gold.read_text()).get(key) if key else None
         got = digest(out.cpu().numpy().view(np.uint32))
         if ref and abs(args.gib - 4.0) < 1e-9:
             ok = all(got[k] == ref[k] for k in ("count", "xor", "crc_of_crcs"))
@@ -324,34 +509,41 @@ def main():
                 "alg_bytes_per_launch": alg_bytes}
 
     extra = {}
-    if rank == 0 and world == 1 and not args.no_extra:
-        other = "fixed4k" if args.workload == "zipf" else "zipf"
-        o2, l2, s2, d2 = make_dataset(other, target, 0)
+    if not args.no_extra and not args.no_c4:
         del arena
-        a2 = torch.empty(int(o2[-1] + l2[-1]) + 64, dtype=torch.uint8, device="cuda")
-        zdbcrc.synth_fill_device(a2, s2)
-        do2, dl2 = torch.from_numpy(o2).cuda(), torch.from_numpy(l2.astype(np.int32)).cuda()
-        out2 = torch.empty(len(l2), dtype=torch.int32, device="cuda")
-        t_settle = time.perf_counter() + args.settle_s / 2
-        while time.perf_counter() < t_settle:
-            for _ in range(4):
+        torch.cuda.empty_cache()
+        log("C4 leg: integrity scan of 64 datafiles per GPU")
+        extra["c4"] = c4_leg(rank, world, args.steps, args.warmup, args.settle_s / 2, barrier)
+        arena = None
+    if rank == 0 and world == 1 and not args.no_extra:
+        for other in [w for w in ("zipf", "fixed4k", "c2u") if w != args.workload]:
+            o2, l2, s2, d2 = make_dataset(other, target, 0)
+            arena = None
+            a2 = torch.empty(int(o2[-1] + l2[-1]) + 64, dtype=torch.uint8, device="cuda")
+            zdbcrc.synth_fill_device(a2, s2)
+            do2, dl2 = torch.from_numpy(o2).cuda(), torch.from_numpy(l2.astype(np.int32)).cuda()
+            out2 = torch.empty(len(l2), dtype=torch.int32, device="cuda")
+            t_settle = time.perf_counter() + args.settle_s / 2
+            while time.perf_counter() < t_settle:
+                for _ in range(4):
+                    zdbcrc.batch_device(a2, do2, dl2, out2)
+                torch.cuda.synchronize()
+            zdbcrc.kernel_stats()
+            zdbcrc.set_timing(True)
+            ta = time.perf_counter()
+            for _ in range(args.steps):
                 zdbcrc.batch_device(a2, do2, dl2, out2)
             torch.cuda.synchronize()
-        zdbcrc.kernel_stats()
-        zdbcrc.set_timing(True)
-        ta = time.perf_counter()
-        for _ in range(args.steps):
-            zdbcrc.batch_device(a2, do2, dl2, out2)
-        torch.cuda.synchronize()
-        tb = time.perf_counter()
-        zdbcrc.set_timing(False)
-        km, kl = zdbcrc.kernel_stats()
-        pb = int(l2.sum())
-        extra[other] = {"desc": d2, "records": len(l2), "gibs": round(pb * args.steps / (tb - ta) / GIB, 2),
-                        "kernel_ms": round(km / max(kl, 1), 4),
-                        "roofline_frac": round((pb + 16 * len(l2)) / (km / max(kl, 1) / 1e3) / 1e9
-                                               / HBM_PEAK_GBS, 4)}
-        del a2
+            tb = time.perf_counter()
+            zdbcrc.set_timing(False)
+            km, kl = zdbcrc.kernel_stats()
+            pb = int(l2.sum())
+            extra[other] = {"desc": d2, "records": len(l2), "gibs": round(pb * args.steps / (tb - ta) / GIB, 2),
+                            "kernel_ms": round(km / max(kl, 1), 4),
+                            "roofline_frac": round((pb + 16 * len(l2)) / (km / max(kl, 1) / 1e3) / 1e9
+                                                   / HBM_PEAK_GBS, 4)}
+            del a2, do2, dl2, out2
+            torch.cuda.empty_cache()
 
     if rank == 0 and world == 1 and not args.no_extra:
         log("end-to-end legs (host memory)")

@@ -15,7 +15,7 @@ reference, built from /root/reference by oracle/Makefile into oracle/_ref/:
                       purpose, each with the reference integrity-check's
                       stdout / stderr / exit code (TZ=UTC)
   digests.json        count / XOR / order-sensitive crc of the per-record
-                      crcs of the full-size bench datasets (C2, C3), so the GPU
+                      crcs of the full-size bench datasets (C2, C3, C4 shard 0), so the GPU
                       can be checked bit-exact at BASELINE sizes
 
 Run in the build container (needs /root/reference):
@@ -191,13 +191,35 @@ def digests(ref: oracle.Reference) -> dict:
     c3 = ref.batch(arena, offs, lens, threads=8)
     out["C3"] = {"seed": C3_SEED, "len_seed": C3_LEN_SEED, "target": 4 << 30, "total_bytes": total,
                  **digest(ref, c3)}
+    del arena
+    out["C4"] = digest_c4(ref)
     return out
+
+
+def digest_c4(ref: oracle.Reference) -> dict:
+    """C4 shard of rank 0 (bench.c4_layout): 64 reference-valid datafiles,
+    ~16 GiB; payload crcs by the reference over the synthetic image bytes
+    (headers never overlap payloads, so they need not be written here)."""
+    import zdbcrc
+    sys.path.insert(0, str(ROOT))
+    import bench
+    lay = bench.c4_layout(0)
+    arena = zdbcrc.synth_fill(lay["total"], bench.C4_SEED)
+    c4 = ref.batch(arena, lay["payload_off"].astype(np.uint64), lay["lens"].astype(np.uint32), threads=8)
+    return {"seed": bench.C4_SEED, "len_seed": bench.C4_LEN_SEED, "files": len(lay["file_off"]),
+            "image_bytes": lay["total"], "payload_bytes": int(lay["lens"].sum()), **digest(ref, c4)}
 
 
 def main():
     ref = oracle.Reference()
     assert ref.engine() == "sse42", ref.engine()
     OUT.mkdir(parents=True, exist_ok=True)
+    if "--only-c4" in sys.argv:  # add / refresh the C4 digest only
+        d = json.loads((OUT / "digests.json").read_text())
+        d["C4"] = digest_c4(ref)
+        (OUT / "digests.json").write_text(json.dumps(d, indent=1) + "\n")
+        print("digests.json C4:", d["C4"])
+        return
     if "--only-digests" in sys.argv:
         d = digests(ref)
         (OUT / "digests.json").write_text(json.dumps(d, indent=1) + "\n")

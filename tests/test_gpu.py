@@ -233,3 +233,52 @@ def test_tool_gpu_engine_matches_reference(tmp_path, datafile_cases, name):
     assert out == eout
     assert err == eerr
     assert code == {c["name"]: c for c in datafile_cases}[name]["exit"]
+
+
+# ------------------------------------------------------------------ C4 -------
+
+def test_c4_device_image_and_verify(dev, oracle_c):
+    """bench.c4_build_device writes the same bytes as the host construction
+    (which the reference tool accepts, tests/test_c4.py), its crcs match the
+    oracle, and verify_device flags exactly the corrupted records."""
+    import bench
+    lay = bench.c4_layout(1, files=3, file_cap=6 << 20)
+    seed = bench.C4_SEED + 1
+    img, poff, plen, expected, crcs = bench.c4_build_device(lay, seed)
+    host = bench.c4_image_host(lay, seed, crcs)
+    np.testing.assert_array_equal(img[: lay["total"]].cpu().numpy(), host)
+    np.testing.assert_array_equal(crcs, oracle_c.batch(host, lay["payload_off"], lay["lens"]))
+    np.testing.assert_array_equal(expected.cpu().numpy().view(np.uint32), crcs)
+    n = len(lay["lens"])
+    out = torch.empty(n, dtype=torch.int32, device="cuda")
+    mism = torch.zeros(64, dtype=torch.int32, device="cuda")
+    cnt = torch.zeros(1, dtype=torch.int32, device="cuda")
+    dev.verify_device(img, poff, plen, expected, out, mism, cnt)
+    torch.cuda.synchronize()
+    assert int(cnt.item()) == 0
+    bad = [r for r in (3, n // 2, n - 1) if lay["lens"][r] > 0]
+    for r in bad:
+        img[int(lay["payload_off"][r]) + int(lay["lens"][r]) // 2] ^= 0x40
+    dev.verify_device(img, poff, plen, expected, out, mism, cnt)
+    torch.cuda.synchronize()
+    assert int(cnt.item()) == len(bad)
+    assert sorted(mism[: len(bad)].cpu().tolist()) == sorted(bad)
+
+
+def test_full_size_c4_shard_digest(dev, digests):
+    """The rank-0 C4 shard (64 datafiles, ~16 GiB in HBM) against the digest
+    the reference computed on the CPU (tests/golden/make_golden.py)."""
+    import bench
+    d = digests["C4"]
+    lay = bench.c4_layout(0)
+    assert lay["total"] == d["image_bytes"] and len(lay["lens"]) == d["count"]
+    img, poff, plen, expected, crcs = bench.c4_build_device(lay, bench.C4_SEED)
+    assert bench.digest(crcs) == {k: d[k] for k in ("count", "xor", "crc_of_crcs")}
+    out = torch.empty(len(crcs), dtype=torch.int32, device="cuda")
+    mism = torch.zeros(16, dtype=torch.int32, device="cuda")
+    cnt = torch.zeros(1, dtype=torch.int32, device="cuda")
+    dev.verify_device(img, poff, plen, expected, out, mism, cnt)
+    torch.cuda.synchronize()
+    assert int(cnt.item()) == 0
+    del img
+    torch.cuda.empty_cache()
