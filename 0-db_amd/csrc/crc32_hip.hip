@@ -347,6 +347,7 @@ __device__ __forceinline__ bool next_seg_batched(uint64_t &r, uint64_t n, uint64
 
 // loads of superstep ss: uniform base (segment's first piece) + 32-bit lane
 // offset; lanes before the segment re-read its first piece (zeroed later)
+template <bool NTL = false, bool NOLOAD = false>
 __device__ __forceinline__ void load_superstep_v3(const SegCtx &s, uint32_t ss, uint32_t lane, uint4 (&buf)[K]) {
     const uint64_t base = s.P0 + 16u * (uint64_t)s.pa;
     const int32_t rel0 = (int32_t)(s.base_j - (int64_t)s.pa) + 64 * (int32_t)(ss * K) + (int32_t)lane;
@@ -354,7 +355,13 @@ __device__ __forceinline__ void load_superstep_v3(const SegCtx &s, uint32_t ss, 
     for (int i = 0; i < K; i++) {
         int32_t rel = rel0 + 64 * i;
         rel = rel < 0 ? 0 : rel;
-        const u32x4 v = *reinterpret_cast<global_u32x4 *>(base + ((uint64_t)(uint32_t)rel << 4));
+        global_u32x4 *p = reinterpret_cast<global_u32x4 *>(base + ((uint64_t)(uint32_t)rel << 4));
+        if (NOLOAD) { // timing diagnostic: no memory traffic, data made up from the address
+            const uint32_t a = (uint32_t)reinterpret_cast<uint64_t>(p);
+            buf[i] = make_uint4(a, a * 0x9E3779B9u, a ^ 0x5bd1e995u, a + ss);
+            continue;
+        }
+        const u32x4 v = NTL ? __builtin_nontemporal_load(p) : *p;
         buf[i] = make_uint4(v.x, v.y, v.z, v.w);
     }
 }
@@ -416,7 +423,10 @@ __device__ __forceinline__ uint64_t block_excl_scan64(uint64_t v, uint64_t *wsum
 // Without it the co-resident waves of a CU finish up to 2x apart (age-ordered
 // arbitration; measured with the STAMP build) and the kernel ends on a tail.
 // NOZ: timing diagnostic only (skips the trailing-pad shift: wrong checksums)
-template <int WGT, int WPE, bool STAMP = false, int PRIO = 0, uint32_t UO = UNIT_OVH, bool NOZ = false>
+// NTL: payload loads carry the nontemporal hint (read once, never reused)
+// NOLOAD: timing diagnostic only (no payload loads: the compute floor; wrong checksums)
+template <int WGT, int WPE, bool STAMP = false, int PRIO = 0, uint32_t UO = UNIT_OVH, bool NOZ = false,
+          bool NTL = false, bool NOLOAD = false>
 __global__ __launch_bounds__(WGT, WPE) void crc_batch_kernel_v3(
     const uint8_t *__restrict__ arena, const uint64_t *__restrict__ offsets,
     const uint32_t *__restrict__ lengths, const PlanArgs plan, uint64_t n,
@@ -475,7 +485,7 @@ __global__ __launch_bounds__(WGT, WPE) void crc_batch_kernel_v3(
         load_meta(m, rn, n, lane, unit_start, arena, offsets, lengths);
         active = next_seg_batched<UO>(rn, n, ub, ue, lane, m, unit_start, arena, offsets, lengths, cur);
         if (active)
-            load_superstep_v3(cur.c, 0, lane, bufc);
+            load_superstep_v3<NTL, NOLOAD>(cur.c, 0, lane, bufc);
     }
     const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     if (PRIO && lane == 0)
@@ -518,7 +528,7 @@ __global__ __launch_bounds__(WGT, WPE) void crc_batch_kernel_v3(
             nx = cur;
             nss = css;
         }
-        load_superstep_v3(nx.c, nss, lane, bufn);
+        load_superstep_v3<NTL, NOLOAD>(nx.c, nss, lane, bufn);
         if (css == 0 || css + 1 == cur.S)
             acc = superstep<true>(cur.c, acc, bufc, css, cur.t0, lane, lds);
         else
@@ -600,6 +610,8 @@ const KernelVariant kVariants[] = {
     {"v3_wg768_stamp", crc_batch_kernel_v3<768, 6, true>, 768},
     {"v3_wg768_prio_ovh16", crc_batch_kernel_v3<768, 6, false, 1, 16>, 768, WG_PER_CU, 16},
     {"v3_wg768_prio_noz", crc_batch_kernel_v3<768, 6, false, 1, UNIT_OVH, true>, 768},
+    {"v3_wg768_prio_nt", crc_batch_kernel_v3<768, 6, false, 1, UNIT_OVH, false, true>, 768},
+    {"v3_wg768_prio_noload", crc_batch_kernel_v3<768, 6, false, 1, UNIT_OVH, false, true, true>, 768},
 };
 
 constexpr int kNumVariants = (int)(sizeof(kVariants) / sizeof(kVariants[0]));
@@ -722,7 +734,7 @@ __global__ __launch_bounds__(256) void stream_read_kernel(const uint4 *__restric
 // contiguous-slice variant of the probe: wave w reads its own slice, 1 KiB
 // per load instruction, U loads per lane per iteration -- the access shape of
 // crc_batch_kernel without any checksum work
-template <int U>
+template <int U, bool NTL = false>
 __global__ __launch_bounds__(1024) void stream_slice_kernel(const uint4 *__restrict__ src, uint64_t words,
                                                             uint32_t *__restrict__ sink) {
     const uint32_t lane = threadIdx.x & 63;
@@ -735,7 +747,12 @@ __global__ __launch_bounds__(1024) void stream_slice_kernel(const uint4 *__restr
         uint4 x[U];
 #pragma unroll
         for (int u = 0; u < U; u++)
-            x[u] = src[i + 64 * u];
+            if (NTL) {
+                const u32x4 t = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(src + i + 64 * u));
+                x[u] = make_uint4(t.x, t.y, t.z, t.w);
+            } else {
+                x[u] = src[i + 64 * u];
+            }
 #pragma unroll
         for (int u = 0; u < U; u++) {
             a.x ^= x[u].x; a.y ^= x[u].y; a.z ^= x[u].z; a.w ^= x[u].w;
@@ -961,12 +978,19 @@ float zdbcrc_debug_stream_read(const void *d_buf, size_t bytes, uint32_t *d_sink
     const uint64_t words = bytes / 16;
     // blocks > 0: grid-stride probe with that many 256-thread blocks;
     // blocks = -U: contiguous-slice probe, 512 x 1024-thread blocks, U loads/lane
+    // blocks = -100 - U: the same with nontemporal loads
     if (blocks > 0)
         hipLaunchKernelGGL(stream_read_kernel, dim3(blocks), dim3(256), 0, st, src, words, d_sink);
     else if (blocks == -4)
         hipLaunchKernelGGL(stream_slice_kernel<4>, dim3(512), dim3(1024), 0, st, src, words, d_sink);
     else if (blocks == -8)
         hipLaunchKernelGGL(stream_slice_kernel<8>, dim3(512), dim3(1024), 0, st, src, words, d_sink);
+    else if (blocks == -104)
+        hipLaunchKernelGGL((stream_slice_kernel<4, true>), dim3(512), dim3(1024), 0, st, src, words, d_sink);
+    else if (blocks == -204)
+        hipLaunchKernelGGL((stream_slice_kernel<4, true>), dim3(512), dim3(768), 0, st, src, words, d_sink);
+    else if (blocks == -108)
+        hipLaunchKernelGGL((stream_slice_kernel<8, true>), dim3(512), dim3(1024), 0, st, src, words, d_sink);
     else
         hipLaunchKernelGGL(stream_slice_kernel<16>, dim3(512), dim3(1024), 0, st, src, words, d_sink);
     hipEventRecord(b, st);

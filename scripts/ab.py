@@ -27,7 +27,7 @@ sink = torch.zeros(1 << 16, dtype=torch.int32, device="cuda")
 st = torch.cuda.current_stream().cuda_stream
 for mib in [int(x) for x in os.environ.get("PROBE_MIB", "4096").split(",") if x]:
     buf = torch.empty(mib << 20, dtype=torch.uint8, device="cuda"); buf.fill_(7)
-    for blocks in (2048, 8192, 16384, -4, -8, -16):
+    for blocks in [int(b) for b in os.environ.get("PROBE_BLOCKS", "2048,8192,16384,-4,-8,-16").split(",")]:
         ts = [probe(buf.data_ptr(), buf.numel(), sink.data_ptr(), blocks, st) for _ in range(6)][1:]
         print(json.dumps({"probe": "stream_read_%dMiB" % mib, "blocks": blocks,
                           "median_ms": round(float(np.median(ts)), 4),
@@ -61,6 +61,13 @@ for wl in work.split(","):
     do, dl = torch.from_numpy(offs).cuda(), torch.from_numpy(lens.astype(np.int32)).cuda()
     outs = {v: torch.empty(len(lens), dtype=torch.int32, device="cuda") for v in sel}
     times = {v: [] for v in sel}
+    # clock settle: ~1 s of untimed launches before the first timed round
+    set_variant(sel[0])
+    t_end = time.time() + float(os.environ.get("SETTLE_S", "1.0"))
+    while time.time() < t_end:
+        for _ in range(20):
+            zdbcrc.batch_device(arena, do, dl, outs[sel[0]])
+        torch.cuda.synchronize()
     for r in range(ROUNDS):
         for v in sel:
             set_variant(v)
