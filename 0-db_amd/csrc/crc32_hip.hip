@@ -74,25 +74,78 @@ __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
     return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96); // a ^ b ^ c in one VALU op
 }
 
-// 5-bit slice c (bits [5c, 5c+5)) of a little-endian 128-bit piece.
-// c is a compile-time constant after unrolling.
-__device__ __forceinline__ uint32_t piece_slice(const uint4 &v, int c) {
-    const int s = 5 * c, d = s >> 5, sh = s & 31;
-    if (sh <= 27 || d == 3)
-        return (word_of(v, d) >> sh) & 31u;
-    return __builtin_amdgcn_alignbit(word_of(v, d + 1), word_of(v, d), sh) & 31u;
+__device__ __forceinline__ uint32_t rotr(uint32_t x, int s) { return __builtin_amdgcn_alignbit(x, x, s); }
+
+// (x on mask m) | (y elsewhere): one v_bfi_b32.  Inline asm so the
+// demanded-bits combiner cannot split it into and/and/or.
+template <uint32_t M>
+__device__ __forceinline__ uint32_t sel(uint32_t x, uint32_t y) {
+    uint32_t r;
+    asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "s"(M), "v"(x), "v"(y));
+    return r;
+}
+
+// dword byte address of the window in byte n of x: bits [8n+2, 8n+7) of x,
+// already scaled by 4 -- one VALU op (v_and_b32, SDWA byte select for n > 0)
+// (the compiler finds the SDWA form for bytes 2 and 3 by itself; byte 1 is
+// spelled out, it would otherwise emit a shift + and)
+__device__ __forceinline__ uint32_t win(uint32_t x, int n) {
+    if (n == 0)
+        return x & 0x7Cu;
+    if (n == 1) {
+        uint32_t r;
+        asm("v_and_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_1 src1_sel:DWORD"
+            : "=v"(r)
+            : "v"(x), "s"(0x7Cu));
+        return r;
+    }
+    return (x >> (8 * n)) & 0x7Cu;
+}
+
+// table entry at byte address a of window j's 32-entry table
+__device__ __forceinline__ uint32_t look(const uint32_t *tab, int j, uint32_t a) {
+    return *reinterpret_cast<const uint32_t *>(reinterpret_cast<const char *>(tab) + j * 128 + a);
 }
 
 // contribution of one piece in slot I of a superstep: 26 conflict-free
-// lookups, folded three at a time (v_bitop3 xor3) in issue order
-template <int I>
+// lookups over the windows of crc32c_gf2.h (zdbcrc_window_bit), 37 VALU ops
+// of index extraction (16 A windows at one op each, two B words at three ops
+// + one per window, the C word at five + one per window), folded three at a
+// time (v_bitop3 xor3)
+// XM (A/B only): 0 = the windows above; 1 = timing diagnostic with one-op
+// extraction for every window (wrong checksums)
+template <int I, int XM = 0>
 __device__ __forceinline__ uint32_t piece_contrib(const uint4 &v, const uint32_t *lds) {
     const uint32_t *tab = lds + ZDBCRC_OFF_T + I * PCH * 32;
-    // 26 lookups folded two per v_bitop3 (three-input XOR)
-    uint32_t r = 0;
+    const uint32_t w0 = v.x, w1 = v.y, w2 = v.z, w3 = v.w;
+    if (XM == 1) { // timing diagnostic: 1-op extraction for all 26 (wrong checksums, same LDS pattern)
+        uint32_t r = 0;
 #pragma unroll
-    for (int c = 0; c < PCH; c += 2)
-        r = xor3(r, tab[c * 32 + piece_slice(v, c)], tab[(c + 1) * 32 + piece_slice(v, c + 1)]);
+        for (int c = 0; c < PCH; c += 2)
+            r = xor3(r, look(tab, c, win(word_of(v, (c >> 2) & 3), c & 3)),
+                     look(tab, c + 1, win(word_of(v, ((c + 1) >> 2) & 3), (c + 1) & 3)));
+        return r;
+    }
+    // A: windows 0..15
+    uint32_t r = xor3(look(tab, 0, win(w0, 0)), look(tab, 1, win(w0, 1)), look(tab, 2, win(w0, 2)));
+    r = xor3(r, look(tab, 3, win(w0, 3)), look(tab, 4, win(w1, 0)));
+    r = xor3(r, look(tab, 5, win(w1, 1)), look(tab, 6, win(w1, 2)));
+    r = xor3(r, look(tab, 7, win(w1, 3)), look(tab, 8, win(w2, 0)));
+    r = xor3(r, look(tab, 9, win(w2, 1)), look(tab, 10, win(w2, 2)));
+    r = xor3(r, look(tab, 11, win(w2, 3)), look(tab, 12, win(w3, 0)));
+    r = xor3(r, look(tab, 13, win(w3, 1)), look(tab, 14, win(w3, 2)));
+    // B: windows 16..23
+    const uint32_t u1 = sel<0x1C1C1C1Cu>(rotr(w0, 29), rotr(w1, 27));
+    const uint32_t u2 = sel<0x1C1C1C1Cu>(rotr(w2, 29), rotr(w3, 27));
+    r = xor3(r, look(tab, 15, win(w3, 3)), look(tab, 16, win(u1, 0)));
+    r = xor3(r, look(tab, 17, win(u1, 1)), look(tab, 18, win(u1, 2)));
+    r = xor3(r, look(tab, 19, win(u1, 3)), look(tab, 20, win(u2, 0)));
+    r = xor3(r, look(tab, 21, win(u2, 1)), look(tab, 22, win(u2, 2)));
+    // C: windows 24, 25 (4 index bits each)
+    const uint32_t z = sel<0x04040404u>(w1 >> 5, w3 >> 4);
+    const uint32_t z2 = sel<0x00300030u>(rotr(z, 6), z);
+    r = xor3(r, look(tab, 23, win(u2, 3)), look(tab, 24, z2 & 0x3Cu));
+    r ^= look(tab, 25, (z2 >> 16) & 0x3Cu);
     return r;
 }
 
@@ -184,7 +237,7 @@ __device__ __forceinline__ uint4 edge_piece(const SegCtx &s, uint4 v, uint32_t t
 // superstep can hold empty leading steps / lanes and the record's first
 // piece; only the last can hold the record's last piece: EDGE enables the
 // checks there, the middle supersteps run without them.
-template <bool EDGE>
+template <bool EDGE, int XM = 0>
 __device__ __forceinline__ uint32_t superstep(const SegCtx &s, uint32_t acc, const uint4 (&cur)[K], uint32_t ss,
                                               uint32_t t0, uint32_t lane, const uint32_t *lds) {
     if (ss)
@@ -192,7 +245,7 @@ __device__ __forceinline__ uint32_t superstep(const SegCtx &s, uint32_t acc, con
     const uint32_t tb = ss * K;
 #define ZDBCRC_SLOT(I)                                                                   \
     if (!EDGE || tb + I >= t0)                                                           \
-        acc ^= piece_contrib<I>(EDGE ? edge_piece(s, cur[I], tb + I, lane) : cur[I], lds);
+        acc ^= piece_contrib<I, XM>(EDGE ? edge_piece(s, cur[I], tb + I, lane) : cur[I], lds);
 
     ZDBCRC_SLOT(0)
     ZDBCRC_SLOT(1)
@@ -426,7 +479,7 @@ __device__ __forceinline__ uint64_t block_excl_scan64(uint64_t v, uint64_t *wsum
 // NTL: payload loads carry the nontemporal hint (read once, never reused)
 // NOLOAD: timing diagnostic only (no payload loads: the compute floor; wrong checksums)
 template <int WGT, int WPE, bool STAMP = false, int PRIO = 0, uint32_t UO = UNIT_OVH, bool NOZ = false,
-          bool NTL = false, bool NOLOAD = false>
+          bool NTL = false, bool NOLOAD = false, int XM = 0>
 __global__ __launch_bounds__(WGT, WPE) void crc_batch_kernel_v3(
     const uint8_t *__restrict__ arena, const uint64_t *__restrict__ offsets,
     const uint32_t *__restrict__ lengths, const PlanArgs plan, uint64_t n,
@@ -530,9 +583,9 @@ __global__ __launch_bounds__(WGT, WPE) void crc_batch_kernel_v3(
         }
         load_superstep_v3<NTL, NOLOAD>(nx.c, nss, lane, bufn);
         if (css == 0 || css + 1 == cur.S)
-            acc = superstep<true>(cur.c, acc, bufc, css, cur.t0, lane, lds);
+            acc = superstep<true, XM>(cur.c, acc, bufc, css, cur.t0, lane, lds);
         else
-            acc = superstep<false>(cur.c, acc, bufc, css, cur.t0, lane, lds);
+            acc = superstep<false, XM>(cur.c, acc, bufc, css, cur.t0, lane, lds);
         uint32_t *dst = dummy;
         uint32_t x = 0;
         if (css + 1 == cur.S) {
@@ -604,14 +657,13 @@ struct KernelVariant {
 
 // selectable with ZDBCRC_VARIANT=<index> (A/B measurement); 0 is the default
 const KernelVariant kVariants[] = {
-    {"v3_wg768_prio", crc_batch_kernel_v3<768, 6, false, 1>, 768},
-    {"v3_wg768", crc_batch_kernel_v3<768, 6>, 768},
-    {"v3_wg768_prio_stamp", crc_batch_kernel_v3<768, 6, true, 1>, 768},
-    {"v3_wg768_stamp", crc_batch_kernel_v3<768, 6, true>, 768},
-    {"v3_wg768_prio_ovh16", crc_batch_kernel_v3<768, 6, false, 1, 16>, 768, WG_PER_CU, 16},
-    {"v3_wg768_prio_noz", crc_batch_kernel_v3<768, 6, false, 1, UNIT_OVH, true>, 768},
     {"v3_wg768_prio_nt", crc_batch_kernel_v3<768, 6, false, 1, UNIT_OVH, false, true>, 768},
+    {"v3_wg768_prio", crc_batch_kernel_v3<768, 6, false, 1>, 768},
+    {"v3_wg768_nt", crc_batch_kernel_v3<768, 6, false, 0, UNIT_OVH, false, true>, 768},
+    {"v3_wg768_prio_nt_stamp", crc_batch_kernel_v3<768, 6, true, 1, UNIT_OVH, false, true>, 768},
+    {"v3_wg768_prio_nt_noz", crc_batch_kernel_v3<768, 6, false, 1, UNIT_OVH, true, true>, 768},
     {"v3_wg768_prio_noload", crc_batch_kernel_v3<768, 6, false, 1, UNIT_OVH, false, true, true>, 768},
+    {"v3_wg768_prio_nt_cheapx", crc_batch_kernel_v3<768, 6, false, 1, UNIT_OVH, false, true, false, 1>, 768},
 };
 
 constexpr int kNumVariants = (int)(sizeof(kVariants) / sizeof(kVariants[0]));

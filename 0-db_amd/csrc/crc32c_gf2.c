@@ -86,13 +86,41 @@ uint32_t zdbcrc_update_bytes(uint32_t crc, const uint8_t *p, size_t n) {
     return crc;
 }
 
-/* crc (from 0) of a 16-byte piece whose only set bits are (v << bit) */
-static uint32_t piece_slice_crc(uint32_t v, int bit) {
+int zdbcrc_window_bit(int j, int t) {
+    if (j < 0 || j >= ZDBCRC_PCH || t < 0 || t >= 5)
+        return -1;
+    if (j < 16) /* A */
+        return 32 * (j >> 2) + 8 * (j & 3) + 2 + t;
+    if (j < 24) { /* B: u = rotl3(w_a) | rotl5(w_b), byte n, bits [2,7) */
+        const int a = j < 20 ? 0 : 2, n = (j - 16) & 3;
+        switch (t) {
+        case 0: return 32 * a + ((8 * n + 31) & 31);
+        case 1: return 32 * a + 8 * n;
+        case 2: return 32 * a + 8 * n + 1;
+        case 3: return 32 * (a + 1) + 8 * n;
+        default: return 32 * (a + 1) + 8 * n + 1;
+        }
+    }
+    /* C: z2 bits [2,6) (j = 24) and [18,22) (j = 25) */
+    {
+        const int m = 2 * (j - 24); /* byte of w1/w3 behind index bits 0,1 */
+        switch (t) {
+        case 0: return 32 + 8 * m + 7;
+        case 1: return 96 + 8 * m + 7;
+        case 2: return 32 + 8 * (m + 1) + 7;
+        case 3: return 96 + 8 * (m + 1) + 7;
+        default: return -1;
+        }
+    }
+}
+
+/* crc (from 0) of a 16-byte piece whose only set bits are window j's bits selected by v */
+static uint32_t piece_window_crc(uint32_t v, int j) {
     uint8_t piece[16];
     memset(piece, 0, sizeof(piece));
-    for (int k = 0; k < 5; k++) {
-        int b = bit + k;
-        if (((v >> k) & 1) && b < 128)
+    for (int t = 0; t < 5; t++) {
+        const int b = zdbcrc_window_bit(j, t);
+        if (((v >> t) & 1) && b >= 0)
             piece[b >> 3] |= (uint8_t)(1u << (b & 7));
     }
     return zdbcrc_update_bytes(0, piece, 16);
@@ -111,7 +139,7 @@ void zdbcrc_build_tables(uint32_t *img) {
         for (int c = 0; c < ZDBCRC_PCH; c++)
             for (uint32_t v = 0; v < 32; v++)
                 img[ZDBCRC_OFF_T + (i * ZDBCRC_PCH + c) * 32 + v] =
-                    zdbcrc_shift(piece_slice_crc(v, 5 * c), 1024 * (int64_t)(ZDBCRC_K - 1 - i));
+                    zdbcrc_shift(piece_window_crc(v, c), 1024 * (int64_t)(ZDBCRC_K - 1 - i));
 
     for (int c = 0; c < ZDBCRC_SCH; c++)
         for (uint32_t v = 0; v < 32; v++)

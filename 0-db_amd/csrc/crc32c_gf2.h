@@ -39,7 +39,7 @@ uint32_t zdbcrc_update_bytes(uint32_t crc, const uint8_t *p, size_t n);
  * group, so a lookup wave-instruction is conflict-free whatever the data.
  */
 #define ZDBCRC_K         4   /* pieces (16 B) per lane per superstep      */
-#define ZDBCRC_PCH      26   /* 5-bit slices of a 128-bit piece (25x5+3)  */
+#define ZDBCRC_PCH      26   /* lookup windows of a 128-bit piece        */
 #define ZDBCRC_SCH       7   /* 5-bit slices of a 32-bit register (6x5+2) */
 #define ZDBCRC_WAVE     64
 #define ZDBCRC_RDIG      4   /* radix-256 digits of a piece count (< 2^32) */
@@ -54,8 +54,28 @@ uint32_t zdbcrc_update_bytes(uint32_t crc, const uint8_t *p, size_t n);
 #define ZDBCRC_TABLE_DW (ZDBCRC_OFF_R + ZDBCRC_RDIG * 256 * ZDBCRC_SCH * 32)
 
 /*
- * T[i][c][v] : crc of a 16-byte piece whose only set bits are v << 5c,
- *              then shifted by 1024*(K-1-i) bytes (slot i of a superstep)
+ * Piece windows.  A 16-byte piece (dwords w0..w3, little endian) is covered
+ * by 26 lookup windows chosen so that the kernel extracts most indices with
+ * ONE VALU op (an SDWA byte select + AND 0x7C gives bits [8n+2, 8n+7) of a
+ * dword already scaled to a dword address):
+ *   j  0..15  A: bits [8n+2, 8n+7) of w_k            (k = j/4, n = j%4)
+ *   j 16..19  B: byte n of u1 = rotl3(w0) on 0x1C1C1C1C | rotl5(w1) elsewhere
+ *   j 20..23  B: byte n of u2, the same from (w2, w3)
+ *              -> index bits: w_a bit 8n-1 (mod 32), 8n, 8n+1, w_b bit 8n, 8n+1
+ *   j 24..25  C: z = (w1 >> 5) on 0x04040404 | (w3 >> 4) elsewhere,
+ *              z2 = rotr6(z) on 0x00300030 | z elsewhere; bits [2,6) and
+ *              [18,22) of z2 -> w1 bit 8m+7, w3 bit 8m+7 for m = 2c', 2c'+1
+ * zdbcrc_window_bit(j, t) is the piece bit behind index bit t of window j
+ * (-1 for the unused 5th bit of the C windows); the tables below are built
+ * from it, and the kernel's extraction (crc32_hip.hip piece_contrib) and the
+ * CPU model (tests/kernel_model.py) follow the same map.
+ */
+int zdbcrc_window_bit(int j, int t);
+
+/*
+ * T[i][j][v] : crc of a 16-byte piece whose only set bits are those of
+ *              window j selected by v, then shifted by 1024*(K-1-i) bytes
+ *              (slot i of a superstep)
  * W[c][v]    : shift(v << 5c, 1024*K)          (register across a superstep)
  * L[c][v][l] : shift(v << 5c, 16*(63-l))       (lane l's final placement)
  * Z[z][c][v] : shift(v << 5c, -z), z = 0..15   (trailing pad removal)

@@ -25,13 +25,29 @@ MIN_UNITS_PER_WAVE = 256
 LANES = np.arange(WAVE, dtype=np.int64)
 
 
+def window_bit(j: int, t: int) -> int:
+    """Piece bit behind index bit t of lookup window j (-1: unused), as
+    zdbcrc_window_bit in 0-db_amd/csrc/crc32c_gf2.c defines the windows."""
+    if j < 16:  # A: bits [8n+2, 8n+7) of dword j/4
+        return 32 * (j >> 2) + 8 * (j & 3) + 2 + t
+    if j < 24:  # B: rotl3(w_a) | rotl5(w_b), byte n
+        a, n = (0 if j < 20 else 2), (j - 16) & 3
+        return [32 * a + ((8 * n + 31) & 31), 32 * a + 8 * n, 32 * a + 8 * n + 1,
+                32 * (a + 1) + 8 * n, 32 * (a + 1) + 8 * n + 1][t]
+    m = 2 * (j - 24)  # C: bit 7 of bytes m, m+1 of w1 and w3
+    return [32 + 8 * m + 7, 96 + 8 * m + 7, 32 + 8 * (m + 1) + 7, 96 + 8 * (m + 1) + 7, -1][t]
+
+
+_WIN = np.array([[window_bit(j, t) for t in range(5)] for j in range(PCH)], dtype=np.int64)
+
+
 def _slices128(words: np.ndarray) -> np.ndarray:
-    """words: [64, 4] uint32 -> [64, 26] 5-bit slices of the 128-bit piece."""
-    w = words.astype(object)
-    big = w[:, 0] | (w[:, 1] << 32) | (w[:, 2] << 64) | (w[:, 3] << 96)
+    """words: [64, 4] uint32 -> [64, 26] window indices of the 128-bit piece."""
+    bits = np.unpackbits(words.astype("<u4").view(np.uint8), axis=1, bitorder="little").astype(np.int64)
     out = np.zeros((len(words), PCH), dtype=np.int64)
-    for c in range(PCH):
-        out[:, c] = [int((b >> (5 * c)) & 31) for b in big]
+    for t in range(5):
+        col = _WIN[:, t]
+        out |= np.where(col >= 0, bits[:, np.maximum(col, 0)], 0) << t
     return out
 
 

@@ -5,6 +5,8 @@ segment splits across waves and the atomic-XOR recombination -- without a
 GPU.  The GPU tests check the HIP implementation of the same algorithm."""
 from __future__ import annotations
 
+import ctypes
+
 import numpy as np
 import pytest
 
@@ -28,11 +30,23 @@ def _case(seed, nrec, maxlen, arena_len):
     return arena, offs, lens
 
 
+def test_windows_cover_every_piece_bit_once():
+    bits = [km.window_bit(j, t) for j in range(km.PCH) for t in range(5)]
+    used = sorted(b for b in bits if b >= 0)
+    assert used == list(range(128))
+    # the library's table builder uses the same map
+    f = zdbcrc._lib.zdbcrc_window_bit
+    f.restype, f.argtypes = ctypes.c_int, [ctypes.c_int, ctypes.c_int]
+    assert [f(j, t) for j in range(km.PCH) for t in range(5)] == bits
+
+
 def test_table_spot_values(tab):
-    # slot K-1 of the data tables is plain crc of a piece with one slice set
-    piece = np.zeros(16, np.uint8)
-    piece[0] = 1
-    assert tab[km.OFF_T + ((km.K - 1) * km.PCH + 0) * 32 + 1] == oracle.crc32_py(piece.tobytes())
+    # slot K-1 of the data tables is plain crc of a piece with one window bit set
+    for j, t in ((0, 0), (5, 3), (16, 0), (23, 4), (24, 1), (25, 3)):
+        b = km.window_bit(j, t)
+        piece = np.zeros(16, np.uint8)
+        piece[b >> 3] = 1 << (b & 7)
+        assert tab[km.OFF_T + ((km.K - 1) * km.PCH + j) * 32 + (1 << t)] == oracle.crc32_py(piece.tobytes())
     # lane 63 is not shifted at all
     for v in range(32):
         assert tab[km.OFF_L + (0 * 32 + v) * 64 + 63] == v
