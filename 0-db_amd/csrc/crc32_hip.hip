@@ -58,6 +58,10 @@ constexpr int WG_PER_CU = 2;              // 2 x 70 KiB of LDS tables per CU
 // 384: 0.765, 512: 0.779; profiles/r1/ab_unit_ovh.jsonl)
 constexpr uint32_t UNIT_OVH = 384;
 constexpr uint64_t MIN_UNITS_PER_WAVE = 256;
+// dword offsets inside the per-stream scratch: [0, 16384) one dummy store
+// word per wave, [16384, 131072) diagnostic stamps, [131072, 132096) per-CU
+// arrival counters (PRIO >= 2)
+constexpr uint32_t SCRATCH_CU_CTR = 131072;
 
 static_assert(ZDBCRC_LDS_DW % 4 == 0, "LDS image must be 16-byte granular");
 static_assert(ZDBCRC_LDS_DW * 4 * WG_PER_CU <= 160 * 1024, "LDS budget");
@@ -118,6 +122,16 @@ template <int I, int XM = 0>
 __device__ __forceinline__ uint32_t piece_contrib(const uint4 &v, const uint32_t *lds) {
     const uint32_t *tab = lds + ZDBCRC_OFF_T + I * PCH * 32;
     const uint32_t w0 = v.x, w1 = v.y, w2 = v.z, w3 = v.w;
+    if (XM == 3) { // timing diagnostic: the 16 A windows only (wrong checksums)
+        uint32_t r = xor3(look(tab, 0, win(w0, 0)), look(tab, 1, win(w0, 1)), look(tab, 2, win(w0, 2)));
+        r = xor3(r, look(tab, 3, win(w0, 3)), look(tab, 4, win(w1, 0)));
+        r = xor3(r, look(tab, 5, win(w1, 1)), look(tab, 6, win(w1, 2)));
+        r = xor3(r, look(tab, 7, win(w1, 3)), look(tab, 8, win(w2, 0)));
+        r = xor3(r, look(tab, 9, win(w2, 1)), look(tab, 10, win(w2, 2)));
+        r = xor3(r, look(tab, 11, win(w2, 3)), look(tab, 12, win(w3, 0)));
+        r = xor3(r, look(tab, 13, win(w3, 1)), look(tab, 14, win(w3, 2)));
+        return r ^ look(tab, 15, win(w3, 3));
+    }
     if (XM == 1) { // timing diagnostic: 1-op extraction for all 26 (wrong checksums, same LDS pattern)
         uint32_t r = 0;
 #pragma unroll
@@ -197,6 +211,24 @@ __device__ __forceinline__ uint4 mask_piece(uint4 v, int lo, int hi) {
     v.z &= keep_mask(lo, hi, 2);
     v.w &= keep_mask(lo, hi, 3);
     return v;
+}
+
+// Pieces of a record of L > 0 bytes at address a.  Normally the 16-byte
+// grid of the address space (aligned loads, first/last piece partial).  When
+// that grid costs the record one more 1 KiB step than a grid starting at the
+// record itself would (a 4 KiB value after a 26-byte datafile header: 257
+// aligned pieces = 5 steps, 256 record-relative pieces = 4), the record uses
+// the record-relative grid instead: its loads are byte-misaligned (≈ 20 %
+// slower to stream, measured) but it saves a fifth of its lookups.  Only for
+// L % 16 == 0, so the last piece ends exactly at the record's end and no load
+// leaves the 16-byte blocks the aligned grid reads anyway.  The planner and
+// the walk both derive the grid from the piece count.
+__host__ __device__ __forceinline__ uint64_t pieces_aligned(uint64_t a, uint64_t L) {
+    return ((a + L - 1) >> 4) - (a >> 4) + 1;
+}
+__host__ __device__ __forceinline__ uint64_t record_pieces(uint64_t a, uint64_t L) {
+    const uint64_t na = pieces_aligned(a, L), nr = L >> 4;
+    return (L & 15) == 0 && ((nr + 63) >> 6) < ((na + 63) >> 6) ? nr : na;
 }
 
 struct SegCtx {
@@ -380,10 +412,13 @@ __device__ __forceinline__ bool next_seg_batched(uint64_t &r, uint64_t n, uint64
             const uint64_t Aend = A + __builtin_amdgcn_readlane(m.len, li);
             sg.r = r;
             sg.us = us;
-            sg.c.P0 = A & ~15ull;
             sg.c.np = (uint32_t)(ur - us);
+            // record-relative grid iff the planner counted fewer pieces than
+            // the aligned grid has (record_pieces)
+            const bool rel = sg.c.np != (uint32_t)pieces_aligned(A, Aend - A);
+            sg.c.P0 = rel ? A : (A & ~15ull);
             sg.z = (uint32_t)(sg.c.P0 + 16u * (uint64_t)sg.c.np - Aend);
-            sg.c.lo0 = (int)(A & 15u);
+            sg.c.lo0 = rel ? 0 : (int)(A & 15u);
             sg.c.hi_last = 16 - (int)sg.z;
             sg.c.pa = (uint32_t)(s_lo - us);
             sg.pb = (uint32_t)(s_hi - us);
@@ -475,6 +510,10 @@ __device__ __forceinline__ uint64_t block_excl_scan64(uint64_t v, uint64_t *wsum
 // superstep and the slower half raises its issue priority (s_setprio 3).
 // Without it the co-resident waves of a CU finish up to 2x apart (age-ordered
 // arbitration; measured with the STAMP build) and the kernel ends on a tail.
+// PRIO 2/3: the same, plus the two workgroups sharing a CU are told apart
+// (arrival order at a per-CU counter, keyed by the hardware CU id): issue
+// arbitration favours the older workgroup, so the younger one runs on a
+// priority one step (2) or two steps (3) above it.
 // NOZ: timing diagnostic only (skips the trailing-pad shift: wrong checksums)
 // NTL: payload loads carry the nontemporal hint (read once, never reused)
 // NOLOAD: timing diagnostic only (no payload loads: the compute floor; wrong checksums)
@@ -545,6 +584,14 @@ __global__ __launch_bounds__(WGT, WPE) void crc_batch_kernel_v3(
         prog[wid] = active ? 0u : 0xFFFFFFFFu; // an idle wave counts as ahead of everyone
     if (lane < 2)
         slot[2 * wid + lane] = ~0u;
+    if (PRIO >= 2 && threadIdx.x == 0) {
+        // arrival order of this workgroup on its CU (parity of a per-CU
+        // counter that every launch advances by the CU's workgroup count)
+        const uint32_t hw = __builtin_amdgcn_s_getreg(0xF804);  // HW_REG_HW_ID
+        const uint32_t xcc = __builtin_amdgcn_s_getreg(0xF814); // HW_REG_XCC_ID
+        const uint32_t key = ((xcc & 7u) << 7) | (((hw >> 13) & 7u) << 5) | (((hw >> 12) & 1u) << 4) | ((hw >> 8) & 15u);
+        prog[15] = atomicAdd(scratch + SCRATCH_CU_CTR + key, 1u) & 1u;
+    }
     {
         const uint4 *src = reinterpret_cast<const uint4 *>(tables);
         uint4 *dst = reinterpret_cast<uint4 *>(lds);
@@ -554,22 +601,50 @@ __global__ __launch_bounds__(WGT, WPE) void crc_batch_kernel_v3(
     __syncthreads();
     if (!active)
         return;
+    const uint32_t young = PRIO >= 2 ? __builtin_amdgcn_readfirstlane(prog[15]) : 0u;
 
     uint32_t *const dummy = scratch + gw;
     uint64_t cut_r[2] = {0, 0};
     uint32_t cut_x[2] = {0, 0}, ncut = 0;
     uint32_t css = 0, acc = 0, iter = 0;
     for (;;) {
-        if (PRIO == 1 && (++iter & 1) == 0) {
+        if (PRIO && (++iter & 1) == 0) {
             const uint32_t mine = (uint32_t)(cur.us + cur.c.pa + 64u * K * css - ub);
             if (lane == 0)
                 prog[wid] = mine;
             const uint32_t other = lane < (uint32_t)(WGT / 64) ? prog[lane] : 0u;
             const uint32_t ahead = (uint32_t)__popcll(__ballot(other > mine));
-            if (ahead >= (uint32_t)(WGT / 128))
-                __builtin_amdgcn_s_setprio(3);
-            else
-                __builtin_amdgcn_s_setprio(0);
+            const bool slow = ahead >= (uint32_t)(WGT / 128);
+            if (PRIO == 1) {
+                if (slow)
+                    __builtin_amdgcn_s_setprio(3);
+                else
+                    __builtin_amdgcn_s_setprio(0);
+            } else if (PRIO == 2) { // older {0, 2}, younger {1, 3}
+                if (slow) {
+                    if (young)
+                        __builtin_amdgcn_s_setprio(3);
+                    else
+                        __builtin_amdgcn_s_setprio(2);
+                } else {
+                    if (young)
+                        __builtin_amdgcn_s_setprio(1);
+                    else
+                        __builtin_amdgcn_s_setprio(0);
+                }
+            } else { // older {0, 1}, younger {2, 3}
+                if (young) {
+                    if (slow)
+                        __builtin_amdgcn_s_setprio(3);
+                    else
+                        __builtin_amdgcn_s_setprio(2);
+                } else {
+                    if (slow)
+                        __builtin_amdgcn_s_setprio(1);
+                    else
+                        __builtin_amdgcn_s_setprio(0);
+                }
+            }
         }
         uint32_t nss = 0;
         bool more = true;
@@ -609,7 +684,7 @@ __global__ __launch_bounds__(WGT, WPE) void crc_batch_kernel_v3(
         for (int i = 0; i < K; i++)
             bufc[i] = bufn[i];
     }
-    if (PRIO == 1 && lane == 0)
+    if (PRIO && lane == 0)
         prog[wid] = 0xFFFFFFFFu; // finished: counts as ahead of everyone
     if (STAMP && lane == 0) {
         uint64_t *st = reinterpret_cast<uint64_t *>(scratch + 16384) + 4 * gw;
@@ -664,6 +739,14 @@ const KernelVariant kVariants[] = {
     {"v3_wg768_prio_nt_noz", crc_batch_kernel_v3<768, 6, false, 1, UNIT_OVH, true, true>, 768},
     {"v3_wg768_prio_noload", crc_batch_kernel_v3<768, 6, false, 1, UNIT_OVH, false, true, true>, 768},
     {"v3_wg768_prio_nt_cheapx", crc_batch_kernel_v3<768, 6, false, 1, UNIT_OVH, false, true, false, 1>, 768},
+    {"v3_wg1024_prio_nt", crc_batch_kernel_v3<1024, 8, false, 1, UNIT_OVH, false, true>, 1024},
+    {"v3_wg768_prio_nt_a16", crc_batch_kernel_v3<768, 6, false, 1, UNIT_OVH, false, true, false, 3>, 768},
+    {"v3_wg768_prio_noload_a16", crc_batch_kernel_v3<768, 6, false, 1, UNIT_OVH, false, true, true, 3>, 768},
+    {"v3_wg768_prio_noload_cheapx", crc_batch_kernel_v3<768, 6, false, 1, UNIT_OVH, false, true, true, 1>, 768},
+    {"v3_wg768_prio2_nt", crc_batch_kernel_v3<768, 6, false, 2, UNIT_OVH, false, true>, 768},
+    {"v3_wg768_prio3_nt", crc_batch_kernel_v3<768, 6, false, 3, UNIT_OVH, false, true>, 768},
+    {"v3_wg768_prio2_nt_stamp", crc_batch_kernel_v3<768, 6, true, 2, UNIT_OVH, false, true>, 768},
+    {"v3_wg768_prio3_nt_stamp", crc_batch_kernel_v3<768, 6, true, 3, UNIT_OVH, false, true>, 768},
 };
 
 constexpr int kNumVariants = (int)(sizeof(kVariants) / sizeof(kVariants[0]));
@@ -693,7 +776,7 @@ struct UnitCount {
         if (!L)
             return ovh;
         const uint64_t a = reinterpret_cast<uint64_t>(arena) + offsets[r];
-        return ovh + (((a + L - 1) >> 4) - (a >> 4) + 1);
+        return ovh + record_pieces(a, L);
     }
 };
 
@@ -720,7 +803,7 @@ __global__ __launch_bounds__(PLAN_T) void plan_kernel(const uint8_t *__restrict_
             uint64_t v = ovh;
             if (L) {
                 const uint64_t a = reinterpret_cast<uint64_t>(arena) + offsets[r];
-                v += ((a + L - 1) >> 4) - (a >> 4) + 1;
+                v += record_pieces(a, L);
             }
             s += v;
             out[r] = 0;
@@ -738,7 +821,7 @@ __global__ __launch_bounds__(PLAN_T) void plan_kernel(const uint8_t *__restrict_
             uint64_t v = ovh;
             if (L) {
                 const uint64_t a = reinterpret_cast<uint64_t>(arena) + offsets[r];
-                v += ((a + L - 1) >> 4) - (a >> 4) + 1;
+                v += record_pieces(a, L);
             }
             e += v;
         }

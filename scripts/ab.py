@@ -9,6 +9,8 @@ import numpy as np
 ROOT = Path(__file__).resolve().parents[1]
 sys.path[:0] = [str(ROOT / "0-db_amd")]
 import torch, zdbcrc
+sys.path.insert(0, str(ROOT))
+import bench
 
 set_variant = zdbcrc._lib.zdbcrc_debug_set_variant
 set_variant.restype = C.c_char_p
@@ -27,23 +29,27 @@ sink = torch.zeros(1 << 16, dtype=torch.int32, device="cuda")
 st = torch.cuda.current_stream().cuda_stream
 for mib in [int(x) for x in os.environ.get("PROBE_MIB", "4096").split(",") if x]:
     buf = torch.empty(mib << 20, dtype=torch.uint8, device="cuda"); buf.fill_(7)
-    for blocks in [int(b) for b in os.environ.get("PROBE_BLOCKS", "2048,8192,16384,-4,-8,-16").split(",")]:
-        ts = [probe(buf.data_ptr(), buf.numel(), sink.data_ptr(), blocks, st) for _ in range(6)][1:]
-        print(json.dumps({"probe": "stream_read_%dMiB" % mib, "blocks": blocks,
+    for spec in [x for x in os.environ.get("PROBE_BLOCKS", "2048,8192,16384,-4,-8,-16").split(",") if x]:
+        # "<blocks>@<misalign>": the same probe over a base address misaligned by that many bytes
+        blocks, mis = (int(x) for x in spec.split("@")) if "@" in spec else (int(spec), 0)
+        ts = [probe(buf.data_ptr() + mis, buf.numel() - 64, sink.data_ptr(), blocks, st) for _ in range(6)][1:]
+        print(json.dumps({"probe": "stream_read_%dMiB" % mib, "blocks": blocks, "misalign": mis,
                           "median_ms": round(float(np.median(ts)), 4),
                           "tbs": round(buf.numel() / (np.median(ts) / 1e3) / 1e12, 3)}), flush=True)
     del buf
 sel = [int(x) for x in sys.argv[2].split(",")] if len(sys.argv) > 2 else list(range(len(names)))
 work = sys.argv[1] if len(sys.argv) > 1 else "zipf"
 ROUNDS, STEPS = 5, 5
-for wl in work.split(","):
+for wl in [w for w in work.split(",") if w and w != "none"]:
     align = 1
     size = 4 << 30
     label = wl
     if "@" in wl:  # e.g. single@128: the same workload scaled to 128 MiB (cache-resident probe)
         wl, mib = wl.split("@")
         size = int(mib) << 20
-    if wl in ("zipf", "zipf16"):
+    if wl in ("zipf", "fixed4k", "c2u"):  # bench.py's workloads, rank-0 datasets
+        offs, lens, seed, _ = bench.make_dataset(wl, size, 0)
+    elif wl == "zipf16":
         lens = zdbcrc.zipf_lengths(size, 0xC3C3C3).astype(np.int64)
         seed = 0x5A0DB5EED + 3
         align = 16 if wl == "zipf16" else 1
@@ -53,8 +59,9 @@ for wl in work.split(","):
         lens = np.full(1 << 16, 65536, np.int64); seed = 0x5A0DB5EED
     else:
         lens = np.full(size >> 12, 4096, np.int64); seed = 0x5A0DB5EED
-    padded = (lens + align - 1) // align * align
-    offs = np.zeros(len(lens), np.int64); offs[1:] = np.cumsum(padded[:-1])
+    if wl not in ("zipf", "fixed4k", "c2u"):
+        padded = (lens + align - 1) // align * align
+        offs = np.zeros(len(lens), np.int64); offs[1:] = np.cumsum(padded[:-1])
     total = int(offs[-1] + lens[-1])
     arena = torch.empty(total + 64, dtype=torch.uint8, device="cuda")
     zdbcrc.synth_fill_device(arena, seed)

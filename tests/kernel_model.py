@@ -120,6 +120,18 @@ def segment_crc(mem: np.ndarray, base_addr: int, P0: int, pa: int, pb: int, np_:
     return int(np.bitwise_xor.reduce(placed))
 
 
+def pieces_aligned(a: int, L: int) -> int:
+    return ((a + L - 1) >> 4) - (a >> 4) + 1
+
+
+def record_pieces(a: int, L: int) -> int:
+    """Piece count of a record (crc32_hip.hip record_pieces): the 16-byte
+    address grid, or the record-relative grid when L % 16 == 0 and that saves
+    a 1 KiB step."""
+    na, nr = pieces_aligned(a, L), L >> 4
+    return nr if (L & 15) == 0 and (nr + 63) >> 6 < (na + 63) >> 6 else na
+
+
 def batch(arena: np.ndarray, offsets, lengths, tab: np.ndarray, max_waves: int = 4096,
           min_units: int = MIN_UNITS_PER_WAVE, base_addr: int = 0) -> np.ndarray:
     """out[r] as crc_batch_kernel computes it.  base_addr is the (virtual)
@@ -137,7 +149,8 @@ def batch(arena: np.ndarray, offsets, lengths, tab: np.ndarray, max_waves: int =
     mem_base = base_addr - pad_lo  # absolute address of mem[0]
 
     A = base_addr + offsets
-    units = np.where(lengths > 0, ((A + lengths - 1) >> 4) - (A >> 4) + 1, 0) + UNIT_OVH
+    units = np.array([record_pieces(int(a), int(L)) if L > 0 else 0 for a, L in zip(A, lengths)],
+                     dtype=np.int64) + UNIT_OVH
     unit_start = np.zeros(n + 1, dtype=np.int64)
     unit_start[1:] = np.cumsum(units)
     total = int(unit_start[n])
@@ -155,11 +168,12 @@ def batch(arena: np.ndarray, offsets, lengths, tab: np.ndarray, max_waves: int =
             if s_hi > s_lo:
                 a = int(A[r])
                 aend = a + int(lengths[r])
-                P0 = a & ~15
                 np_ = ur - us
+                rel = np_ != pieces_aligned(a, aend - a)
+                P0 = a if rel else a & ~15
                 z = P0 + 16 * np_ - aend
                 pa, pb = s_lo - us, s_hi - us
-                x = segment_crc(mem, mem_base, P0, pa, pb, np_, a & 15, 16 - z, tab)
+                x = segment_crc(mem, mem_base, P0, pa, pb, np_, 0 if rel else a & 15, 16 - z, tab)
                 if z:
                     x = _uniform_shift(x, tab, OFF_Z + z * SCH * 32)
                 x = shift_pieces(x, np_ - pb, tab)

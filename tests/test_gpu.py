@@ -89,6 +89,23 @@ def test_random_batches(dev, oracle_c, seed, nrec, maxlen):
     np.testing.assert_array_equal(gpu_batch(dev, arena, offs, lens), oracle_c.batch(arena, offs, lens))
 
 
+def test_record_relative_grid(dev, oracle_c):
+    """1 KiB-multiple records at misaligned addresses (the 4 KiB value after a
+    26-byte datafile header) take the record-relative piece grid and
+    byte-misaligned loads; mixed with records of nearby lengths that keep the
+    aligned grid, cut across many waves."""
+    rng = np.random.default_rng(31)
+    base = [1024, 2048, 4096, 8192, 65536, 1 << 20]
+    lens = np.concatenate([rng.choice(base, 3000), rng.choice([4080, 4095, 4097, 4112, 1008, 16], 600)])
+    rng.shuffle(lens)
+    gaps = rng.integers(0, 40, len(lens))
+    offs = np.zeros(len(lens), np.int64)
+    offs[1:] = np.cumsum(lens[:-1] + gaps[:-1])
+    offs += 26
+    arena = oracle.splitmix_bytes(int(offs[-1] + lens[-1]) + 16, 31)
+    np.testing.assert_array_equal(gpu_batch(dev, arena, offs, lens), oracle_c.batch(arena, offs, lens))
+
+
 def test_overlapping_and_empty(dev, oracle_c):
     arena = oracle.splitmix_bytes(100_000, 77)
     offs = [0, 0, 1, 0, 50_000, 99_999, 12_345, 12_345]

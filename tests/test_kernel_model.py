@@ -83,3 +83,17 @@ def test_radix_shift_tables(tab):
     for q in [1, 255, 256, 257, 65535, 65536, 1 << 24, (1 << 28) + 1, 0xFFFFFFFF]:
         x = int(rng.integers(1, 1 << 32))
         assert km.shift_pieces(x, q, tab) == zdbcrc.shift(x, 16 * q)
+
+
+def test_record_relative_grid(oracle_c, tab):
+    # 1 KiB-multiple records at misaligned addresses take the record-relative
+    # piece grid (one step fewer); neighbours of other lengths stay aligned
+    arena = oracle.splitmix_bytes(30_000, 33)
+    lens = [4096, 1024, 2048, 4096 - 16, 4096 + 16, 1000, 4096, 17]
+    offs = [26, 4200, 5301, 7400, 11533, 16000, 17013, 21111]
+    for r, (o, L) in enumerate(zip(offs, lens)):
+        if L % 1024 == 0 and o % 16:
+            assert km.record_pieces(o, L) == L // 16 < km.pieces_aligned(o, L)
+    for mw, mu in ((4096, 256), (7, 1)):
+        got = km.batch(arena, offs, lens, tab, max_waves=mw, min_units=mu)
+        np.testing.assert_array_equal(got, oracle_c.batch(arena, offs, lens))
