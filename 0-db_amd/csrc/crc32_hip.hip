@@ -743,6 +743,9 @@ const KernelVariant kVariants[] = {
     {"v3_wg768_prio_nt_a16", crc_batch_kernel_v3<768, 6, false, 1, UNIT_OVH, false, true, false, 3>, 768},
     {"v3_wg768_prio_noload_a16", crc_batch_kernel_v3<768, 6, false, 1, UNIT_OVH, false, true, true, 3>, 768},
     {"v3_wg768_prio_noload_cheapx", crc_batch_kernel_v3<768, 6, false, 1, UNIT_OVH, false, true, true, 1>, 768},
+    {"v3_wg1024_prio_noload", crc_batch_kernel_v3<1024, 8, false, 1, UNIT_OVH, false, true, true>, 1024},
+    {"v3_wg512_prio_noload", crc_batch_kernel_v3<512, 4, false, 1, UNIT_OVH, false, true, true>, 512},
+    {"v3_wg512_prio_nt", crc_batch_kernel_v3<512, 4, false, 1, UNIT_OVH, false, true>, 512},
     {"v3_wg768_prio2_nt", crc_batch_kernel_v3<768, 6, false, 2, UNIT_OVH, false, true>, 768},
     {"v3_wg768_prio3_nt", crc_batch_kernel_v3<768, 6, false, 3, UNIT_OVH, false, true>, 768},
     {"v3_wg768_prio2_nt_stamp", crc_batch_kernel_v3<768, 6, true, 2, UNIT_OVH, false, true>, 768},
@@ -900,6 +903,41 @@ __global__ __launch_bounds__(1024) void stream_slice_kernel(const uint4 *__restr
     uint32_t v = wave_xor(a.x ^ a.y ^ a.z ^ a.w);
     if (lane == 0)
         atomicXor(sink + (w & 0xFFFF), v);
+}
+
+// LDS lookup microbenchmark (measurement aid): every lane does ITERS rounds
+// of 16 independent table lookups (5-bit indices from a per-lane xorshift
+// state, V VALU ops of index extraction per lookup) into 32-entry tables,
+// XOR-folded; B64: ds_read_b64 of 8-byte entries instead of ds_read_b32
+template <int V, bool B64>
+__global__ __launch_bounds__(768, 6) void lds_bench_kernel(uint32_t iters, uint32_t *__restrict__ sink) {
+    __shared__ __attribute__((aligned(16))) uint32_t tab[16 * 64];
+    for (int i = threadIdx.x; i < 16 * 64; i += blockDim.x)
+        tab[i] = i * 0x9E3779B9u;
+    __syncthreads();
+    uint32_t x = (blockIdx.x * blockDim.x + threadIdx.x) * 0x85EBCA6Bu + 1u, acc = 0;
+    for (uint32_t it = 0; it < iters; it++) {
+        uint32_t r = 0;
+#pragma unroll
+        for (int k = 0; k < 16; k++) {
+            const uint32_t w = k < 8 ? x : acc ^ x;
+            uint32_t a;
+            if (V == 1)
+                a = (w >> (4 * (k & 7))) & (B64 ? 0xF8u : 0x7Cu);
+            else
+                a = ((w >> (3 * (k & 7) + 1)) & 31u) << (B64 ? 3 : 2);
+            if (B64) {
+                const uint2 e = *reinterpret_cast<const uint2 *>(reinterpret_cast<const char *>(tab) + k * 256 + a);
+                r = xor3(r, e.x, e.y);
+            } else {
+                r ^= *reinterpret_cast<const uint32_t *>(reinterpret_cast<const char *>(tab) + k * 128 + a);
+            }
+        }
+        acc ^= r;
+        x ^= x << 13; x ^= x >> 17; x ^= x << 5;
+    }
+    if (acc == 0x12345678u)
+        sink[0] = x;
 }
 
 __device__ __forceinline__ uint64_t mix64(uint64_t z) {
@@ -1128,6 +1166,30 @@ float zdbcrc_debug_stream_read(const void *d_buf, size_t bytes, uint32_t *d_sink
         hipLaunchKernelGGL((stream_slice_kernel<8, true>), dim3(512), dim3(1024), 0, st, src, words, d_sink);
     else
         hipLaunchKernelGGL(stream_slice_kernel<16>, dim3(512), dim3(1024), 0, st, src, words, d_sink);
+    hipEventRecord(b, st);
+    float ms = -1;
+    if (hipEventSynchronize(b) == hipSuccess)
+        hipEventElapsedTime(&ms, a, b);
+    hipEventDestroy(a);
+    hipEventDestroy(b);
+    return ms;
+}
+
+// measurement hook: LDS lookup microbenchmark, mode 0..3 = (V 1|2) x (b32|b64);
+// returns ms for one launch of 2 x 768-thread workgroups per CU
+float zdbcrc_debug_lds_bench(int mode, uint32_t iters, uint32_t *d_sink, int cus, void *stream) {
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    hipEvent_t a, b;
+    hipEventCreate(&a);
+    hipEventCreate(&b);
+    hipEventRecord(a, st);
+    const dim3 grid(2 * cus), blk(768);
+    switch (mode) {
+    case 0: hipLaunchKernelGGL((lds_bench_kernel<1, false>), grid, blk, 0, st, iters, d_sink); break;
+    case 1: hipLaunchKernelGGL((lds_bench_kernel<2, false>), grid, blk, 0, st, iters, d_sink); break;
+    case 2: hipLaunchKernelGGL((lds_bench_kernel<1, true>), grid, blk, 0, st, iters, d_sink); break;
+    default: hipLaunchKernelGGL((lds_bench_kernel<2, true>), grid, blk, 0, st, iters, d_sink); break;
+    }
     hipEventRecord(b, st);
     float ms = -1;
     if (hipEventSynchronize(b) == hipSuccess)
