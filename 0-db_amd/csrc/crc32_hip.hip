@@ -37,6 +37,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <atomic>
 #include <map>
 #include <mutex>
 #include <vector>
@@ -977,10 +978,15 @@ struct DeviceCtx {
     std::map<void *, Workspace> ws; // per stream
 };
 
+// Locking: one mutex per device serialises that device's context,
+// workspaces and host staging (calls on different devices -- one host thread
+// per GPU in the multi-file scan -- run concurrently); g_mu guards the
+// process-wide measurement state (timing events, variant selection).
 std::mutex g_mu;
+std::mutex g_dev_mu[64];
 uint32_t *g_last_scratch = nullptr;
 DeviceCtx g_dev[64];
-bool g_hip_touched = false;
+std::atomic<bool> g_hip_touched{false};
 bool g_timing = false;
 std::vector<std::pair<hipEvent_t, hipEvent_t>> g_pending;
 double g_time_ms = 0;
@@ -997,11 +1003,16 @@ std::vector<uint32_t> &host_tables() {
     return t;
 }
 
-int ensure_device(DeviceCtx **out_ctx, int *out_dev) {
+// the calling thread's current HIP device (the device a call runs on)
+int current_device(int *dev) {
     g_hip_touched = true;
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64)
+    if (hipGetDevice(dev) != hipSuccess || *dev < 0 || *dev >= 64)
         return ZDB_CRC32_ENODEV;
+    return ZDB_CRC32_OK;
+}
+
+// caller holds g_dev_mu[dev]
+int ensure_device(int dev, DeviceCtx **out_ctx) {
     DeviceCtx &c = g_dev[dev];
     if (!c.ready) {
         hipDeviceProp_t prop;
@@ -1022,12 +1033,11 @@ int ensure_device(DeviceCtx **out_ctx, int *out_dev) {
         c.ready = true;
     }
     *out_ctx = &c;
-    *out_dev = dev;
     return ZDB_CRC32_OK;
 }
 
 
-// enqueue memset + plan scan + main kernel; caller holds g_mu
+// enqueue plan + main kernel; caller holds the device's g_dev_mu
 // d_unit_start: the per-record unit prefix when the caller already has it
 // (host-planned batches); nullptr -> computed on the device by the scan
 int enqueue_batch(DeviceCtx &c, const uint8_t *arena, const uint64_t *offsets, const uint32_t *lengths,
@@ -1062,7 +1072,7 @@ int enqueue_batch(DeviceCtx &c, const uint8_t *arena, const uint64_t *offsets, c
     }
     // scratch first: its offset must not move with n
     uint32_t *scratch = static_cast<uint32_t *>(w.ptr);
-    g_last_scratch = scratch;
+    g_last_scratch = scratch; // diagnostics only (single-threaded measurement scripts)
     PlanArgs plan{d_unit_start, nullptr, 0, 0};
     if (!d_unit_start) {
         uint8_t *base = static_cast<uint8_t *>(w.ptr) + scratch_bytes;
@@ -1080,7 +1090,9 @@ int enqueue_batch(DeviceCtx &c, const uint8_t *arena, const uint64_t *offsets, c
     const uint32_t grid = (uint32_t)(c.cus * kv.wgs_per_cu);
     const uint32_t max_waves = grid * (uint32_t)(kv.threads / 64);
     hipEvent_t e0 = nullptr, e1 = nullptr;
+    std::unique_lock<std::mutex> tl(g_mu, std::defer_lock);
     if (g_timing) {
+        tl.lock();
         for (hipEvent_t *e : {&e0, &e1}) {
             if (!g_event_pool.empty()) {
                 *e = g_event_pool.back();
@@ -1095,7 +1107,7 @@ int enqueue_batch(DeviceCtx &c, const uint8_t *arena, const uint64_t *offsets, c
                        out, c.d_tables, max_waves, scratch, ++c.epoch);
     if (hipGetLastError() != hipSuccess)
         return ZDB_CRC32_ELAUNCH;
-    if (g_timing) {
+    if (e1) {
         hipEventRecord(e1, st);
         g_pending.emplace_back(e0, e1);
     }
@@ -1130,10 +1142,11 @@ const char *zdb_crc32_strerror(int code) {
 }
 
 const char *zdb_crc32_batch_engine(void) {
-    std::lock_guard<std::mutex> g(g_mu);
-    for (auto &c : g_dev)
-        if (c.ready)
+    for (int d = 0; d < 64; d++) {
+        std::lock_guard<std::mutex> g(g_dev_mu[d]);
+        if (g_dev[d].ready)
             return "hip-gfx950";
+    }
     return "uninitialized";
 }
 
@@ -1223,11 +1236,13 @@ int zdb_crc32_batch_device(const uint8_t *d_arena, const uint64_t *d_offsets, co
         return ZDB_CRC32_OK;
     if (!d_arena || !d_offsets || !d_lengths || !d_out)
         return ZDB_CRC32_EINVAL;
-    std::lock_guard<std::mutex> g(g_mu);
-    DeviceCtx *c;
     int dev;
-    int rc = ensure_device(&c, &dev);
+    int rc = current_device(&dev);
     if (rc)
+        return rc;
+    std::lock_guard<std::mutex> g(g_dev_mu[dev]);
+    DeviceCtx *c;
+    if ((rc = ensure_device(dev, &c)))
         return rc;
     return enqueue_batch(*c, d_arena, d_offsets, d_lengths, d_out, n, static_cast<hipStream_t>(stream));
 }
@@ -1239,11 +1254,13 @@ int zdb_crc32_verify_device(const uint8_t *d_arena, const uint64_t *d_offsets, c
         return ZDB_CRC32_EINVAL;
     hipStream_t st = static_cast<hipStream_t>(stream);
     {
-        std::lock_guard<std::mutex> g(g_mu);
-        DeviceCtx *c;
         int dev;
-        int rc = ensure_device(&c, &dev);
+        int rc = current_device(&dev);
         if (rc)
+            return rc;
+        std::lock_guard<std::mutex> g(g_dev_mu[dev]);
+        DeviceCtx *c;
+        if ((rc = ensure_device(dev, &c)))
             return rc;
         if (hipMemsetAsync(d_mismatch_count, 0, sizeof(uint32_t), st) != hipSuccess)
             return ZDB_CRC32_ELAUNCH;
@@ -1270,11 +1287,13 @@ int zdb_crc32_batch(const uint8_t *arena, size_t arena_len, const uint64_t *offs
     for (size_t r = 0; r < n; r++)
         if (offsets[r] + lengths[r] > arena_len)
             return ZDB_CRC32_EINVAL;
-    std::lock_guard<std::mutex> g(g_mu);
-    DeviceCtx *c;
     int dev;
-    int rc = ensure_device(&c, &dev);
+    int rc = current_device(&dev);
     if (rc)
+        return rc;
+    std::lock_guard<std::mutex> g(g_dev_mu[dev]);
+    DeviceCtx *c;
+    if ((rc = ensure_device(dev, &c)))
         return rc;
     HostStaging &h = g_host_staging[dev];
     if (!h.st && hipStreamCreateWithFlags(&h.st, hipStreamNonBlocking) != hipSuccess)
@@ -1335,6 +1354,21 @@ int zdb_crc32_batch(const uint8_t *arena, size_t arena_len, const uint64_t *offs
         return ZDB_CRC32_ELAUNCH;
     std::memcpy(out, hout, n * 4);
     return ZDB_CRC32_OK;
+}
+
+int zdb_crc32_device_count(void) {
+    g_hip_touched = true;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess)
+        return 0;
+    return n;
+}
+
+int zdb_crc32_use_device(int device) {
+    g_hip_touched = true;
+    if (device < 0 || device >= 64)
+        return ZDB_CRC32_EINVAL;
+    return hipSetDevice(device) == hipSuccess ? ZDB_CRC32_OK : ZDB_CRC32_ENODEV;
 }
 
 void *zdb_crc32_host_alloc(size_t bytes) {

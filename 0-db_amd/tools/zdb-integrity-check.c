@@ -2,21 +2,34 @@
  * zdb-integrity-check -- GPU counterpart of 0-db's tools/integrity-check.
  *
  * Same command line, stdout, stderr and exit status as the reference tool
- * (tools/integrity-check/integrity-check.c:30-166), but restructured for the
- * MI355X: the datafile is read into memory with one large read, the host walks
- * the entry headers (zdb_datafile_walk), every payload checksum is computed in
- * ONE batched GPU call (zdb_crc32_batch -> crc32_hip.hip), and the report is
- * formatted in a single buffer.  The reference does 4 syscalls and ~7 printf
- * per record around one CPU crc each (integrity-check.c:59-105).
+ * (tools/integrity-check/integrity-check.c:30-166) for one datafile, but
+ * restructured for the MI355X: the datafile is read into pinned memory with
+ * large reads, the host walks the entry headers (zdb_datafile_walk), every
+ * payload checksum is computed in ONE batched GPU call (zdb_crc32_batch ->
+ * crc32_hip.hip), and the report is formatted in a single buffer.  The
+ * reference does 4 syscalls and ~7 printf per record around one CPU crc each
+ * (integrity-check.c:59-105).
  *
- *   usage: zdb-integrity-check [--engine=hip|cpu] <dir>/zdb-data-<id>
+ *   usage: zdb-integrity-check [--engine=hip|cpu] [--jobs=J] [--gpus=G]
+ *                              <dir>/zdb-data-<id> [<dir>/zdb-data-<id> ...]
  *
  * --engine=cpu selects the scalar drop-in engine (zdb_crc32, crc32_cpu.c)
  * explicitly, e.g. to time the reference-compatible CPU path.  The default
  * engine is the GPU; if it cannot run, the tool says so and exits 1 -- it
  * never falls back silently.
  *
- * Observable behaviour mirrored from the reference:
+ * Several datafiles (the store-wide scan): each file's
+ * report is exactly what one reference run on that file prints, and the
+ * reports appear in argument order.  J worker threads (default: 1 for one
+ * file, min(files, 8) otherwise) each read, walk and checksum whole files
+ * concurrently; worker w runs its batches on GPU w mod G (default G = every
+ * visible GPU) -- datafiles are independent (records never span files,
+ * api.c:300-303), so the scan shards with no device-to-device exchange.  The
+ * exit status is the total mismatch count over all files (the reference's
+ * per-file status, summed); a fatal error in one file (zdb_diep: short header
+ * or payload, exit 1) ends the run after the reports of the files before it.
+ *
+ * Observable behaviour mirrored from the reference, per file:
  *   - the argument must exist and its basename start with "zdb-data-"
  *     (:121-133), but the file actually read is "<dir>/d<id>" (data.c:135);
  *   - header validation messages (data.c:197-206) go to stdout with the
@@ -26,20 +39,21 @@
  *     records with datalength 0 are not checked (:81-82);
  *   - a short header or payload read ends the run via zdb_diep (exit 1) with
  *     a message carrying strerror(errno) -- errno is whatever the last failing
- *     libc call left (in practice the localtime() zone lookup), SURVEY App.A.6;
+ *     libc call left in a fresh process (in practice the time-zone lookup of
+ *     the first localtime(), captured once at start-up), SURVEY App.A.6;
  *   - exit status = number of mismatches (:162-165), reported as
  *     "[-] data file inconsistency: %d error(s)".
  *
  * Linking: the header walk and the scalar engine are linked in statically;
- * libzdbcrc.so (HIP) is dlopen'ed only when the GPU engine is about to run,
- * after the header report, so the HIP runtime's own start-up (which touches
- * the time-zone state) happens where the reference's process does nothing.
+ * libzdbcrc.so (HIP) is dlopen'ed only when the GPU engine is first needed.
  */
 #define _GNU_SOURCE
 #include <dlfcn.h>
 #include <errno.h>
 #include <fcntl.h>
 #include <libgen.h>
+#include <pthread.h>
+#include <stdarg.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -56,21 +70,9 @@
 #define COLOR_YELLOW "\033[33;1m"
 #define COLOR_RESET "\033[0m"
 
-static struct timeval g_inittime;
+#define FATAL_EXIT 0x100 /* result flag: the reference process would have exited here */
 
-static void timelog(FILE *fp) {
-    struct timeval n;
-    gettimeofday(&n, NULL);
-    double v = (double)(n.tv_usec - g_inittime.tv_usec) / 1000000 + (double)(n.tv_sec - g_inittime.tv_sec);
-    fprintf(fp, "[% 15.6f]", v);
-}
-
-static void warnp(const char *str, int err) {
-    timelog(stderr);
-    fprintf(stderr, COLOR_YELLOW "[-] %s: %s" COLOR_RESET "\n", str, strerror(err));
-}
-
-/* ---- report buffer ------------------------------------------------------ */
+/* ---- per-file report: stdout bytes with stderr lines anchored in them ---- */
 
 typedef struct {
     char *p;
@@ -80,7 +82,7 @@ typedef struct {
 static void ob_reserve(outbuf_t *b, size_t more) {
     if (b->n + more <= b->cap)
         return;
-    size_t cap = b->cap ? b->cap * 2 : (1u << 20);
+    size_t cap = b->cap ? b->cap * 2 : (1u << 16);
     while (cap < b->n + more)
         cap *= 2;
     b->p = realloc(b->p, cap);
@@ -91,11 +93,22 @@ static void ob_reserve(outbuf_t *b, size_t more) {
     b->cap = cap;
 }
 
-static void ob_str(outbuf_t *b, const char *s) {
-    size_t l = strlen(s);
+static void ob_mem(outbuf_t *b, const char *s, size_t l) {
     ob_reserve(b, l);
     memcpy(b->p + b->n, s, l);
     b->n += l;
+}
+
+static void ob_str(outbuf_t *b, const char *s) { ob_mem(b, s, strlen(s)); }
+
+static void ob_printf(outbuf_t *b, const char *fmt, ...) {
+    char tmp[8192];
+    va_list ap;
+    va_start(ap, fmt);
+    int l = vsnprintf(tmp, sizeof(tmp), fmt, ap);
+    va_end(ap);
+    if (l > 0)
+        ob_mem(b, tmp, (size_t)l < sizeof(tmp) ? (size_t)l : sizeof(tmp) - 1);
 }
 
 static void ob_u64(outbuf_t *b, uint64_t v) {
@@ -126,10 +139,79 @@ static void ob_hex32(outbuf_t *b, uint32_t v, int width) {
         b->p[b->n++] = tmp[--i];
 }
 
-static void ob_flush(outbuf_t *b) {
-    if (b->n)
-        fwrite(b->p, 1, b->n, stdout);
-    b->n = 0;
+typedef struct {
+    outbuf_t out;   /* everything the file's run writes to stdout            */
+    outbuf_t err;   /* everything it writes to stderr, line after line       */
+    size_t *anchor; /* anchor[i]: stdout bytes written before stderr line i  */
+    size_t *eend;   /* eend[i]: end of stderr line i in err                  */
+    size_t nerr, cap_err;
+    int status;     /* errors for this file, | FATAL_EXIT (exit code in low bits) */
+    struct timeval t0; /* the file's zdb_inittime (elapsed-time prefix origin) */
+} report_t;
+
+static void rep_err(report_t *r, const char *fmt, ...) {
+    if (r->nerr == r->cap_err) {
+        r->cap_err = r->cap_err ? 2 * r->cap_err : 16;
+        r->anchor = realloc(r->anchor, r->cap_err * sizeof(size_t));
+        r->eend = realloc(r->eend, r->cap_err * sizeof(size_t));
+        if (!r->anchor || !r->eend) {
+            perror("realloc");
+            exit(EXIT_FAILURE);
+        }
+    }
+    char tmp[8192];
+    va_list ap;
+    va_start(ap, fmt);
+    int l = vsnprintf(tmp, sizeof(tmp), fmt, ap);
+    va_end(ap);
+    if (l > 0)
+        ob_mem(&r->err, tmp, (size_t)l < sizeof(tmp) ? (size_t)l : sizeof(tmp) - 1);
+    r->anchor[r->nerr] = r->out.n;
+    r->eend[r->nerr] = r->err.n;
+    r->nerr++;
+}
+
+/* write the report to the real streams, keeping the stdout/stderr order */
+static void rep_emit(report_t *r) {
+    size_t pos = 0, epos = 0;
+    for (size_t i = 0; i < r->nerr; i++) {
+        if (r->anchor[i] > pos)
+            fwrite(r->out.p + pos, 1, r->anchor[i] - pos, stdout);
+        pos = r->anchor[i];
+        fflush(stdout);
+        fwrite(r->err.p + epos, 1, r->eend[i] - epos, stderr);
+        epos = r->eend[i];
+    }
+    if (r->out.n > pos)
+        fwrite(r->out.p + pos, 1, r->out.n - pos, stdout);
+    fflush(stdout);
+}
+
+static void rep_free(report_t *r) {
+    free(r->out.p);
+    free(r->err.p);
+    free(r->anchor);
+    free(r->eend);
+    memset(r, 0, sizeof(*r));
+}
+
+static double elapsed(const report_t *r) {
+    struct timeval n;
+    gettimeofday(&n, NULL);
+    return (double)(n.tv_usec - r->t0.tv_usec) / 1000000 + (double)(n.tv_sec - r->t0.tv_sec);
+}
+
+/* zdb_warnp (libzdb.c:110-115): elapsed-time prefix, yellow, strerror */
+static void rep_warnp(report_t *r, const char *str, int err) {
+    rep_err(r, "[% 15.6f]" COLOR_YELLOW "[-] %s: %s" COLOR_RESET "\n", elapsed(r), str, strerror(err));
+}
+
+/* zdb_danger (libzdb.h:152) to stdout */
+static void rep_danger(report_t *r, const char *fmt, const char *a, int b, int c) {
+    ob_printf(&r->out, "[% 15.6f]", elapsed(r));
+    ob_str(&r->out, COLOR_RED);
+    ob_printf(&r->out, fmt, a, b, c);
+    ob_str(&r->out, COLOR_RESET "\n");
 }
 
 /* ---- GPU engine, resolved at run time ------------------------------------ */
@@ -138,9 +220,18 @@ typedef struct {
     int (*batch)(const uint8_t *, size_t, const uint64_t *, const uint32_t *, uint32_t *, size_t);
     const char *(*strerror)(int);
     void *(*host_alloc)(size_t);
+    void (*host_free)(void *);
+    int (*device_count)(void);
+    int (*use_device)(int);
 } gpu_api_t;
 
-static int load_gpu(gpu_api_t *api) {
+static gpu_api_t g_gpu;
+static int g_gpu_ok = -1; /* -1 not tried, 0 failed, 1 loaded */
+static int g_gpu_count = 0;
+static pthread_once_t g_gpu_once = PTHREAD_ONCE_INIT;
+
+static void load_gpu_once(void) {
+    g_gpu_ok = 0;
     const char *env = getenv("ZDBCRC_LIB");
     char path[4096];
     if (env) {
@@ -149,165 +240,186 @@ static int load_gpu(gpu_api_t *api) {
         char exe[4096];
         ssize_t n = readlink("/proc/self/exe", exe, sizeof(exe) - 1);
         if (n <= 0)
-            return -1;
+            return;
         exe[n] = 0;
         snprintf(path, sizeof(path), "%s/../lib/libzdbcrc.so", dirname(exe));
     }
     void *h = dlopen(path, RTLD_NOW | RTLD_LOCAL);
     if (!h) {
         fprintf(stderr, "[-] zdb-integrity-check: cannot load %s: %s\n", path, dlerror());
-        return -1;
+        return;
     }
-    api->batch = (int (*)(const uint8_t *, size_t, const uint64_t *, const uint32_t *, uint32_t *,
-                          size_t))dlsym(h, "zdb_crc32_batch");
-    api->strerror = (const char *(*)(int))dlsym(h, "zdb_crc32_strerror");
-    api->host_alloc = (void *(*)(size_t))dlsym(h, "zdb_crc32_host_alloc");
-    return (api->batch && api->strerror && api->host_alloc) ? 0 : -1;
+    g_gpu.batch = (int (*)(const uint8_t *, size_t, const uint64_t *, const uint32_t *, uint32_t *,
+                           size_t))dlsym(h, "zdb_crc32_batch");
+    g_gpu.strerror = (const char *(*)(int))dlsym(h, "zdb_crc32_strerror");
+    g_gpu.host_alloc = (void *(*)(size_t))dlsym(h, "zdb_crc32_host_alloc");
+    g_gpu.host_free = (void (*)(void *))dlsym(h, "zdb_crc32_host_free");
+    g_gpu.device_count = (int (*)(void))dlsym(h, "zdb_crc32_device_count");
+    g_gpu.use_device = (int (*)(int))dlsym(h, "zdb_crc32_use_device");
+    if (!g_gpu.batch || !g_gpu.strerror || !g_gpu.host_alloc || !g_gpu.host_free || !g_gpu.device_count ||
+        !g_gpu.use_device)
+        return;
+    g_gpu_count = g_gpu.device_count();
+    g_gpu_ok = g_gpu_count > 0;
 }
 
-/* ---- file loading --------------------------------------------------------- */
+/* ---- scan configuration and per-worker state ----------------------------- */
 
-static uint8_t *load_file(int fd, size_t *len, const gpu_api_t *gpu, int *read_errno) {
-    struct stat sb;
-    *read_errno = 0;
-    if (fstat(fd, &sb) != 0) {
-        *read_errno = errno;
-        return NULL;
-    }
-    size_t size = (size_t)sb.st_size;
-    uint8_t *buf = gpu ? gpu->host_alloc(size + 16) : malloc(size + 16);
-    if (!buf) {
-        *read_errno = ENOMEM;
-        return NULL;
-    }
-    size_t got = 0;
-    while (got < size) {
-        ssize_t r = read(fd, buf + got, size - got);
-        if (r < 0) {
-            *read_errno = errno;
-            break;
-        }
-        if (r == 0)
-            break;
-        got += (size_t)r;
-    }
-    *len = got;
-    return buf;
+typedef struct {
+    int use_gpu;
+    int gpus;          /* devices to spread the workers over (0 = all)        */
+    int stale_errno;   /* errno a fresh process has after its first localtime */
+} config_t;
+
+typedef struct {
+    int id;
+    int device;        /* -1 until the thread has bound its GPU               */
+    uint8_t *buf;      /* file image (pinned when the GPU engine is used)     */
+    size_t cap;
+} worker_t;
+
+static uint8_t *worker_buffer(worker_t *w, const config_t *cfg, size_t size) {
+    if (w->cap >= size)
+        return w->buf;
+    if (w->buf)
+        cfg->use_gpu ? g_gpu.host_free(w->buf) : free(w->buf);
+    size_t cap = size + (size >> 3) + 4096;
+    w->buf = cfg->use_gpu ? g_gpu.host_alloc(cap) : malloc(cap);
+    w->cap = w->buf ? cap : 0;
+    return w->buf;
 }
 
-static void usage(const char *prog) {
-    fprintf(stderr, "Usage: %s data-filename\n", prog);
-    exit(EXIT_FAILURE);
-}
+/* ---- one datafile, as one reference run would report it ---------------- */
 
-int main(int argc, char *argv[]) {
-    int use_gpu = 1;
-    int argi = 1;
-    while (argi < argc && strncmp(argv[argi], "--", 2) == 0) {
-        if (!strcmp(argv[argi], "--engine=cpu"))
-            use_gpu = 0;
-        else if (!strcmp(argv[argi], "--engine=hip"))
-            use_gpu = 1;
-        else
-            usage(argv[0]);
-        argi++;
-    }
-    if (argc - argi < 1)
-        usage(argv[0]);
-
-    char *filename = argv[argi];
-    printf("[+] checking data integrity of: %s\n", filename);
+static void check_file(const config_t *cfg, worker_t *w, const char *filename, report_t *r) {
+    gettimeofday(&r->t0, NULL);
+    ob_printf(&r->out, "[+] checking data integrity of: %s\n", filename);
 
     struct stat sb;
     if (stat(filename, &sb) != 0 || S_ISDIR(sb.st_mode)) {
-        fprintf(stderr, "[-] %s: invalid target file\n", filename);
-        exit(EXIT_FAILURE);
+        rep_err(r, "[-] %s: invalid target file\n", filename);
+        r->status = FATAL_EXIT | EXIT_FAILURE;
+        return;
     }
-
-    char *filedir = dirname(strdup(filename));
-    char *datafile = basename(filename);
+    char *dup1 = strdup(filename), *dup2 = strdup(filename);
+    const char *filedir = dirname(dup1);
+    const char *datafile = basename(dup2);
     if (strncmp(datafile, "zdb-data-", 9)) {
-        fprintf(stderr, "[-] integrity-check: data filename seems wrong\n");
-        exit(EXIT_FAILURE);
+        rep_err(r, "[-] integrity-check: data filename seems wrong\n");
+        r->status = FATAL_EXIT | EXIT_FAILURE;
+        free(dup1);
+        free(dup2);
+        return;
     }
     uint32_t dataid = (uint32_t)atoi(datafile + 9);
-
-    printf("[+] datafile path: %s\n", filedir);
-    printf("[+] datafile name: %s\n", datafile);
-    printf("[+] datafile id  : %d\n", (int)dataid);
-    gettimeofday(&g_inittime, NULL);
+    ob_printf(&r->out, "[+] datafile path: %s\n", filedir);
+    ob_printf(&r->out, "[+] datafile name: %s\n", datafile);
+    ob_printf(&r->out, "[+] datafile id  : %d\n", (int)dataid);
+    gettimeofday(&r->t0, NULL);
 
     /* the file actually read is <dir>/d<id> (data.c:135) */
     char path[4096];
     snprintf(path, sizeof(path), "%s/d%u", filedir, dataid);
-    int errors = 0;
+    free(dup1);
+    free(dup2);
     int fd = open(path, O_RDONLY);
     if (fd < 0) {
-        warnp(path, errno);
-        errors = 1;
-        fflush(stdout);
-        fprintf(stderr, "[-] data file inconsistency: %d error(s)\n", errors);
-        return errors;
+        rep_warnp(r, path, errno);
+        rep_err(r, "[-] data file inconsistency: %d error(s)\n", 1);
+        r->status = 1;
+        return;
     }
 
-    /* descriptor load + validate (data.c:177-209), before anything touches
-     * the GPU so that errno evolves as in the reference process */
+    /* descriptor load + validate (data.c:177-209) */
     uint8_t hdr[ZDB_DATA_HEADER_SIZE];
     if (pread(fd, hdr, sizeof(hdr), 0) != (ssize_t)sizeof(hdr)) {
         close(fd);
-        fflush(stdout);
-        fprintf(stderr, "[-] data file inconsistency: %d error(s)\n", 1);
-        return 1;
+        rep_err(r, "[-] data file inconsistency: %d error(s)\n", 1);
+        r->status = 1;
+        return;
     }
     uint32_t version;
     memcpy(&version, hdr + 4, 4);
     if (memcmp(hdr, "DAT0", 4)) {
-        timelog(stdout);
-        printf(COLOR_RED "[-] %s: invalid header, wrong magic" COLOR_RESET "\n", path);
-        fflush(stdout);
-        fprintf(stderr, "[-] data file inconsistency: %d error(s)\n", 1);
-        return 1;
+        close(fd);
+        rep_danger(r, "[-] %s: invalid header, wrong magic", path, 0, 0);
+        rep_err(r, "[-] data file inconsistency: %d error(s)\n", 1);
+        r->status = 1;
+        return;
     }
     if (version != ZDB_DATAFILE_VERSION) {
-        timelog(stdout);
-        printf(COLOR_RED "[-] %s: unsupported version detected" COLOR_RESET "\n", path);
-        timelog(stdout);
-        printf(COLOR_RED "[-] file version: %d, supported version: %d" COLOR_RESET "\n", (int)version,
-               ZDB_DATAFILE_VERSION);
-        fflush(stdout);
-        fprintf(stderr, "[-] data file inconsistency: %d error(s)\n", 1);
-        return 1;
+        close(fd);
+        rep_danger(r, "[-] %s: unsupported version detected", path, 0, 0);
+        ob_printf(&r->out, "[% 15.6f]", elapsed(r));
+        ob_printf(&r->out, COLOR_RED "[-] file version: %d, supported version: %d" COLOR_RESET "\n", (int)version,
+                  ZDB_DATAFILE_VERSION);
+        rep_err(r, "[-] data file inconsistency: %d error(s)\n", 1);
+        r->status = 1;
+        return;
     }
 
     uint64_t created, opened;
     memcpy(&created, hdr + 8, 8);
     memcpy(&opened, hdr + 16, 8);
     char datestr[64];
-    printf("[+] integrity-check: header seems correct\n");
+    struct tm tmv;
+    ob_str(&r->out, "[+] integrity-check: header seems correct\n");
     /* zdb_header_date takes a uint32_t epoch (libzdb.c:156) */
-    errno = 0;
     time_t t = (time_t)(uint32_t)created;
-    strftime(datestr, sizeof(datestr), "%F %T", localtime(&t));
-    printf("[+] integrity-check: created at: %s\n", datestr);
+    strftime(datestr, sizeof(datestr), "%F %T", localtime_r(&t, &tmv));
+    ob_printf(&r->out, "[+] integrity-check: created at: %s\n", datestr);
     t = (time_t)(uint32_t)opened;
-    strftime(datestr, sizeof(datestr), "%F %T", localtime(&t));
-    printf("[+] integrity-check: last open: %s\n", datestr);
-    const int stale_errno = errno; /* what zdb_diep would report below */
+    strftime(datestr, sizeof(datestr), "%F %T", localtime_r(&t, &tmv));
+    ob_printf(&r->out, "[+] integrity-check: last open: %s\n", datestr);
 
-    gpu_api_t gpu = {0};
-    if (use_gpu && load_gpu(&gpu) != 0) {
-        fflush(stdout);
-        fprintf(stderr, "[-] zdb-integrity-check: GPU engine unavailable (use --engine=cpu)\n");
-        return EXIT_FAILURE;
+    if (cfg->use_gpu) {
+        pthread_once(&g_gpu_once, load_gpu_once);
+        if (g_gpu_ok != 1) {
+            close(fd);
+            rep_err(r, "[-] zdb-integrity-check: GPU engine unavailable (use --engine=cpu)\n");
+            r->status = FATAL_EXIT | EXIT_FAILURE;
+            return;
+        }
+        if (w->device < 0) {
+            const int ndev = cfg->gpus > 0 && cfg->gpus < g_gpu_count ? cfg->gpus : g_gpu_count;
+            w->device = w->id % ndev;
+            int rc = g_gpu.use_device(w->device);
+            if (rc) {
+                close(fd);
+                rep_err(r, "[-] zdb-integrity-check: GPU %d: %s (use --engine=cpu)\n", w->device,
+                        g_gpu.strerror(rc));
+                r->status = FATAL_EXIT | EXIT_FAILURE;
+                return;
+            }
+        }
     }
 
+    /* whole file in large reads */
     size_t len = 0;
     int read_errno = 0;
-    uint8_t *image = load_file(fd, &len, use_gpu ? &gpu : NULL, &read_errno);
+    uint8_t *image = NULL;
+    if (fstat(fd, &sb) != 0) {
+        read_errno = errno;
+    } else if (!(image = worker_buffer(w, cfg, (size_t)sb.st_size + 16))) {
+        read_errno = ENOMEM;
+    } else {
+        const size_t size = (size_t)sb.st_size;
+        while (len < size) {
+            ssize_t got = pread(fd, image + len, size - len > (64u << 20) ? (64u << 20) : size - len, (off_t)len);
+            if (got < 0) {
+                read_errno = errno;
+                break;
+            }
+            if (got == 0)
+                break;
+            len += (size_t)got;
+        }
+    }
     close(fd);
-    if (!image) {
-        warnp(path, read_errno);
-        return EXIT_FAILURE;
+    if (read_errno) {
+        rep_warnp(r, path, read_errno);
+        r->status = FATAL_EXIT | EXIT_FAILURE;
+        return;
     }
 
     /* header walk -> descriptors */
@@ -320,17 +432,17 @@ int main(int argc, char *argv[]) {
     long nfull = (status == ZDB_WALK_SHORT_PAYLOAD) ? nrec - 1 : nrec;
     uint64_t *offs = malloc(sizeof(uint64_t) * (size_t)(nfull + 1));
     uint32_t *lens = malloc(sizeof(uint32_t) * (size_t)(nfull + 1));
-    uint32_t *idx = malloc(sizeof(uint32_t) * (size_t)(nfull + 1));
     uint32_t *crc = malloc(sizeof(uint32_t) * (size_t)(nfull + 1));
-    size_t m = zdb_datafile_payloads(recs, (size_t)nfull, offs, lens, NULL, idx);
+    size_t m = zdb_datafile_payloads(recs, (size_t)nfull, offs, lens, NULL, NULL);
+    int errors = 0;
     if (m) {
-        if (use_gpu) {
-            int rc = gpu.batch(image, len, offs, lens, crc, m);
+        if (cfg->use_gpu) {
+            int rc = g_gpu.batch(image, len, offs, lens, crc, m);
             if (rc) {
-                fflush(stdout);
-                fprintf(stderr, "[-] zdb-integrity-check: GPU engine failed: %s (use --engine=cpu)\n",
-                        gpu.strerror(rc));
-                return EXIT_FAILURE;
+                rep_err(r, "[-] zdb-integrity-check: GPU engine failed: %s (use --engine=cpu)\n",
+                        g_gpu.strerror(rc));
+                r->status = FATAL_EXIT | EXIT_FAILURE;
+                goto out;
             }
         } else {
             for (size_t i = 0; i < m; i++)
@@ -338,59 +450,188 @@ int main(int argc, char *argv[]) {
         }
     }
 
-    outbuf_t ob = {0};
+    outbuf_t *ob = &r->out;
     size_t k = 0;
     for (long i = 0; i < nrec; i++) {
-        const zdb_record_t *r = &recs[i];
-        const uint8_t *h = image + r->header_offset;
-        ob_str(&ob, "[+] data entry: ");
-        ob_u64(&ob, (uint64_t)(i + 1));
-        ob_str(&ob, ", id length: ");
-        ob_u64(&ob, r->idlength);
-        ob_str(&ob, "\n[+]   expected length: ");
-        ob_u64(&ob, r->datalength);
-        ob_str(&ob, ", current offset: ");
-        ob_u64(&ob, r->header_offset);
-        ob_str(&ob, "\n[+]   previous offset: ");
-        ob_u64(&ob, r->previous);
-        ob_str(&ob, "\n[+]   expected crc   : ");
-        ob_hex32(&ob, r->integrity, 8);
-        ob_str(&ob, "\n[+]   entry flags    : 0x");
-        ob_hex32(&ob, r->flags, 1);
-        ob_str(&ob, "\n[+]   entry key      : 0x");
-        ob_reserve(&ob, 2u * r->idlength + 1);
-        for (uint32_t b = 0; b < r->idlength; b++) {
-            ob.p[ob.n++] = hexdig[h[ZDB_ENTRY_HEADER_SIZE + b] >> 4];
-            ob.p[ob.n++] = hexdig[h[ZDB_ENTRY_HEADER_SIZE + b] & 15];
+        const zdb_record_t *e = &recs[i];
+        const uint8_t *h = image + e->header_offset;
+        ob_str(ob, "[+] data entry: ");
+        ob_u64(ob, (uint64_t)(i + 1));
+        ob_str(ob, ", id length: ");
+        ob_u64(ob, e->idlength);
+        ob_str(ob, "\n[+]   expected length: ");
+        ob_u64(ob, e->datalength);
+        ob_str(ob, ", current offset: ");
+        ob_u64(ob, e->header_offset);
+        ob_str(ob, "\n[+]   previous offset: ");
+        ob_u64(ob, e->previous);
+        ob_str(ob, "\n[+]   expected crc   : ");
+        ob_hex32(ob, e->integrity, 8);
+        ob_str(ob, "\n[+]   entry flags    : 0x");
+        ob_hex32(ob, e->flags, 1);
+        ob_str(ob, "\n[+]   entry key      : 0x");
+        ob_reserve(ob, 2u * e->idlength + 1);
+        for (uint32_t b = 0; b < e->idlength; b++) {
+            ob->p[ob->n++] = hexdig[h[ZDB_ENTRY_HEADER_SIZE + b] >> 4];
+            ob->p[ob->n++] = hexdig[h[ZDB_ENTRY_HEADER_SIZE + b] & 15];
         }
-        ob.p[ob.n++] = '\n';
+        ob->p[ob->n++] = '\n';
 
-        if (r->datalength == 0)
+        if (e->datalength == 0)
             continue;
         if (i >= nfull) { /* short payload: zdb_diep (integrity-check.c:87-88) */
-            ob_flush(&ob);
-            fflush(stdout);
-            warnp("payload entry read failed", stale_errno);
-            exit(EXIT_FAILURE);
+            rep_warnp(r, "payload entry read failed", cfg->stale_errno);
+            r->status = FATAL_EXIT | EXIT_FAILURE;
+            goto out;
         }
-        if (crc[k] != r->integrity) {
-            ob_flush(&ob);
-            fflush(stdout);
-            fprintf(stderr, "[-] integrity check failed: %08x <> %08x\n", crc[k], r->integrity);
+        if (crc[k] != e->integrity) {
+            rep_err(r, "[-] integrity check failed: %08x <> %08x\n", crc[k], e->integrity);
             errors += 1;
         } else {
-            ob_str(&ob, "[+]   data crc       : ok, match\n");
+            ob_str(ob, "[+]   data crc       : ok, match\n");
         }
         k++;
     }
-    ob_flush(&ob);
     if (status == ZDB_WALK_SHORT_HEADER) { /* integrity-check.c:68-69 */
-        fflush(stdout);
-        warnp("data header read failed", stale_errno);
-        exit(EXIT_FAILURE);
+        rep_warnp(r, "data header read failed", cfg->stale_errno);
+        r->status = FATAL_EXIT | EXIT_FAILURE;
+        goto out;
     }
-    fflush(stdout);
     if (errors)
-        fprintf(stderr, "[-] data file inconsistency: %d error(s)\n", errors);
-    return errors;
+        rep_err(r, "[-] data file inconsistency: %d error(s)\n", errors);
+    r->status = errors;
+out:
+    free(recs);
+    free(offs);
+    free(lens);
+    free(crc);
+}
+
+/* ---- the scan: J workers, reports emitted in argument order ------------- */
+
+typedef struct {
+    const config_t *cfg;
+    char **files;
+    int nfiles;
+    report_t *reports;
+    int *done;
+    int next;
+    int stop; /* a fatal report was produced: files after it are not needed */
+    pthread_mutex_t mu;
+    pthread_cond_t cv;
+} scan_t;
+
+typedef struct {
+    scan_t *scan;
+    worker_t w;
+} worker_arg_t;
+
+static void *worker_main(void *p) {
+    worker_arg_t *a = p;
+    scan_t *s = a->scan;
+    for (;;) {
+        pthread_mutex_lock(&s->mu);
+        int i = s->stop ? s->nfiles : s->next++;
+        pthread_mutex_unlock(&s->mu);
+        if (i >= s->nfiles)
+            break;
+        check_file(s->cfg, &a->w, s->files[i], &s->reports[i]);
+        pthread_mutex_lock(&s->mu);
+        s->done[i] = 1;
+        if (s->reports[i].status & FATAL_EXIT)
+            s->stop = 1;
+        pthread_cond_broadcast(&s->cv);
+        pthread_mutex_unlock(&s->mu);
+    }
+    if (a->w.buf)
+        s->cfg->use_gpu ? g_gpu.host_free(a->w.buf) : free(a->w.buf);
+    return NULL;
+}
+
+static void usage(const char *prog) {
+    fprintf(stderr, "Usage: %s data-filename\n", prog);
+    exit(EXIT_FAILURE);
+}
+
+int main(int argc, char *argv[]) {
+    config_t cfg = {1, 0, 0};
+    int jobs = 0;
+    int argi = 1;
+    while (argi < argc && strncmp(argv[argi], "--", 2) == 0) {
+        if (!strcmp(argv[argi], "--engine=cpu"))
+            cfg.use_gpu = 0;
+        else if (!strcmp(argv[argi], "--engine=hip"))
+            cfg.use_gpu = 1;
+        else if (!strncmp(argv[argi], "--jobs=", 7) && atoi(argv[argi] + 7) > 0)
+            jobs = atoi(argv[argi] + 7);
+        else if (!strncmp(argv[argi], "--gpus=", 7) && atoi(argv[argi] + 7) > 0)
+            cfg.gpus = atoi(argv[argi] + 7);
+        else
+            usage(argv[0]);
+        argi++;
+    }
+    if (argc - argi < 1)
+        usage(argv[0]);
+
+    /* errno of a fresh process after its first time-zone lookup (what the
+     * reference's zdb_diep reports for short reads, SURVEY App.A.6) */
+    {
+        errno = 0;
+        time_t t = 0;
+        localtime(&t);
+        localtime(&t);
+        cfg.stale_errno = errno;
+    }
+
+    scan_t s;
+    memset(&s, 0, sizeof(s));
+    s.cfg = &cfg;
+    s.files = argv + argi;
+    s.nfiles = argc - argi;
+    s.reports = calloc((size_t)s.nfiles, sizeof(report_t));
+    s.done = calloc((size_t)s.nfiles, sizeof(int));
+    pthread_mutex_init(&s.mu, NULL);
+    pthread_cond_init(&s.cv, NULL);
+    if (jobs <= 0)
+        jobs = s.nfiles < 8 ? s.nfiles : 8;
+    if (jobs > s.nfiles)
+        jobs = s.nfiles;
+
+    worker_arg_t *wa = calloc((size_t)jobs, sizeof(worker_arg_t));
+    pthread_t *th = calloc((size_t)jobs, sizeof(pthread_t));
+    for (int j = 0; j < jobs; j++) {
+        wa[j].scan = &s;
+        wa[j].w.id = j;
+        wa[j].w.device = -1;
+    }
+    if (jobs == 1) {
+        worker_main(&wa[0]); /* one file or --jobs=1: no extra thread */
+    } else {
+        for (int j = 0; j < jobs; j++)
+            pthread_create(&th[j], NULL, worker_main, &wa[j]);
+    }
+
+    long total = 0;
+    for (int i = 0; i < s.nfiles; i++) {
+        pthread_mutex_lock(&s.mu);
+        while (!s.done[i])
+            pthread_cond_wait(&s.cv, &s.mu);
+        pthread_mutex_unlock(&s.mu);
+        report_t *r = &s.reports[i];
+        rep_emit(r);
+        const int st = r->status;
+        rep_free(r);
+        if (st & FATAL_EXIT) {
+            /* zdb_diep / exit(EXIT_FAILURE) in the reference run; _exit: other
+             * workers may still be inside a GPU call, no teardown under them */
+            fflush(stdout);
+            fflush(stderr);
+            _exit(st & 0xFF);
+        }
+        total += st;
+    }
+    if (jobs > 1)
+        for (int j = 0; j < jobs; j++)
+            pthread_join(th[j], NULL);
+    return (int)(total > 0x7FFFFFFF ? 0x7FFFFFFF : total);
 }

@@ -89,7 +89,8 @@ EXPORTED = [
     "zdb_crc32_engine_value", "zdb_crc32", "zdb_checksum_crc32", "zdb_crc32_shift",
     "zdb_crc32_combine", "zdb_crc32_table_image", "zdb_crc32_strerror", "zdb_crc32_batch_engine",
     "zdb_crc32_gpu_initialized", "zdb_crc32_batch_device", "zdb_crc32_verify_device",
-    "zdb_crc32_batch", "zdb_crc32_host_alloc", "zdb_crc32_host_free", "zdb_crc32_set_timing",
+    "zdb_crc32_batch", "zdb_crc32_device_count", "zdb_crc32_use_device", "zdb_crc32_host_alloc",
+    "zdb_crc32_host_free", "zdb_crc32_set_timing",
     "zdb_crc32_kernel_stats", "zdb_synth_fill", "zdb_synth_fill_device", "zdb_synth_zipf_lengths",
     "zdb_datafile_walk", "zdb_datafile_encode_entry", "zdb_datafile_encode_header",
     "zdb_datafile_payloads", "zdb_datafile_encode_batch",

@@ -96,6 +96,14 @@ int zdb_crc32_verify_device(const uint8_t *d_arena, const uint64_t *d_offsets,
 int zdb_crc32_batch(const uint8_t *arena, size_t arena_len, const uint64_t *offsets,
                     const uint32_t *lengths, uint32_t *out, size_t n);
 
+/* Number of usable HIP devices (initialises HIP; 0 when there is none). */
+int zdb_crc32_device_count(void);
+
+/* Bind the calling thread's batched calls to device `device` (HIP's
+ * per-thread current device; one host thread per GPU for multi-GPU scans --
+ * calls on different devices run concurrently). */
+int zdb_crc32_use_device(int device);
+
 /* pinned host staging for the host-buffer path */
 void *zdb_crc32_host_alloc(size_t bytes);
 void zdb_crc32_host_free(void *p);

@@ -1,0 +1,77 @@
+"""zdb-integrity-check over several datafiles in one run (the
+store-wide scan): every file's report is byte-identical to the reference
+tool's run on that file (tests/golden/datafiles/*), reports come out in
+argument order whatever the number of worker threads, the exit status is the
+summed mismatch count, and a fatal file (short header / payload: zdb_diep in
+the reference) ends the run after the reports of the files before it.
+Scalar engine here; the GPU engine runs the same checks in tests/test_gpu.py."""
+from __future__ import annotations
+
+import os
+import shutil
+import subprocess
+from pathlib import Path
+
+import pytest
+
+from conftest import GOLDEN
+from test_tool_cpu import TIMELOG, TOOL, expected
+
+MULTI = ["mixed", "corrupt_payload", "zipf_small", "multi_errors", "bad_magic", "fixed_4k", "header_only",
+         "corrupt_crc", "bad_version"]
+
+
+def stage(names, tmp: Path):
+    dirs = []
+    for i, name in enumerate(names):
+        d = tmp / f"{i:03d}_{name}"
+        d.mkdir()
+        shutil.copy(GOLDEN / "datafiles" / f"{name}.d0", d / "d0")
+        os.symlink("d0", d / "zdb-data-0")
+        dirs.append(d)
+    return dirs
+
+
+def run_multi(names, tmp: Path, engine: str, extra=()):
+    dirs = stage(names, tmp)
+    p = subprocess.run([str(TOOL), f"--engine={engine}", *extra] + [str(d / "zdb-data-0") for d in dirs],
+                       capture_output=True, env=dict(os.environ, TZ="UTC"), timeout=300)
+    out, err = p.stdout.decode(), p.stderr.decode()
+    for d in dirs:
+        out, err = out.replace(str(d), "@DIR@"), err.replace(str(d), "@DIR@")
+    return TIMELOG.sub("[T]", out), TIMELOG.sub("[T]", err), p.returncode
+
+
+def check_multi(names, tmp: Path, engine: str, cases, extra=()):
+    """the run's output == the reference's per-file outputs concatenated"""
+    exits = {c["name"]: c["exit"] for c in cases}
+    out, err, code = run_multi(names, tmp, engine, extra)
+    eout = "".join(expected(n)[0] for n in names)
+    eerr = "".join(expected(n)[1] for n in names)
+    assert out == eout
+    assert err == eerr
+    assert code == sum(exits[n] for n in names) % 256
+
+
+@pytest.mark.parametrize("jobs", [1, 3, 16])
+def test_multi_file_scan_cpu(tmp_path, datafile_cases, jobs):
+    check_multi(MULTI, tmp_path, "cpu", datafile_cases, [f"--jobs={jobs}"])
+
+
+def test_multi_file_default_jobs_same_file_many_times(tmp_path, datafile_cases):
+    check_multi(["multi_errors"] * 12, tmp_path, "cpu", datafile_cases)
+
+
+@pytest.mark.parametrize("fatal", ["truncated_payload", "truncated_header"])
+def test_fatal_file_ends_the_run(tmp_path, fatal):
+    names = ["mixed", "corrupt_crc", fatal, "multi_errors", "zipf_small"]
+    out, err, code = run_multi(names, tmp_path, "cpu", ["--jobs=4"])
+    # reports of the files up to and including the fatal one, nothing after it
+    assert out == "".join(expected(n)[0] for n in names[:3])
+    assert err == "".join(expected(n)[1] for n in names[:3])
+    assert code == 1
+
+
+def test_bad_option_is_usage_error(tmp_path):
+    p = subprocess.run([str(TOOL), "--jobs=0", str(tmp_path / "zdb-data-0")], capture_output=True)
+    assert p.returncode == 1 and b"Usage:" in p.stderr
