@@ -381,6 +381,33 @@ def e2e_legs(offs, lens, seed) -> dict:
                 assert p.returncode == 0, (name, p.stderr[-500:])
             ic[name + "_s"] = round(min(ts), 4)
         res["integrity_check_256MiB"] = ic
+
+        # store-wide scan: 8 datafiles in one tool run, worker
+        # threads sharing the GPU, against the reference tool run once per file
+        files = []
+        for i in range(8):
+            d = f"{td}/ns{i}"
+            os.mkdir(d)
+            os.link(f"{td}/d0", f"{d}/d0")
+            os.symlink("d0", f"{d}/zdb-data-0")
+            files.append(f"{d}/zdb-data-0")
+        tool = str(ROOT / "0-db_amd/bin/zdb-integrity-check")
+        scan = {"files": len(files), "file_bytes": 28 + len(body)}
+        runs = {"gpu_tool_jobs8": [[tool, "--jobs=8"] + files],
+                "scalar_engine_tool_jobs8": [[tool, "--engine=cpu", "--jobs=8"] + files]}
+        if oracle.REF_INTEGRITY.exists():
+            runs["reference_tool_per_file"] = [[str(oracle.REF_INTEGRITY), f] for f in files]
+        for name, cmds in runs.items():
+            ts = []
+            for _ in range(3):
+                t0 = time.perf_counter()
+                for cmd in cmds:
+                    p = subprocess.run(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, timeout=300)
+                    assert p.returncode == 0, (name, p.stderr[-500:])
+                ts.append(time.perf_counter() - t0)
+            scan[name + "_s"] = round(min(ts), 4)
+            scan[name + "_gibs"] = round(len(files) * (28 + len(body)) / min(ts) / GIB, 2)
+        res["integrity_scan_8x256MiB"] = scan
     return res
 
 

@@ -29,7 +29,7 @@ sink = torch.zeros(1 << 16, dtype=torch.int32, device="cuda")
 st = torch.cuda.current_stream().cuda_stream
 for mib in [int(x) for x in os.environ.get("PROBE_MIB", "4096").split(",") if x]:
     buf = torch.empty(mib << 20, dtype=torch.uint8, device="cuda"); buf.fill_(7)
-    for spec in [x for x in os.environ.get("PROBE_BLOCKS", "2048,8192,16384,-4,-8,-16").split(",") if x]:
+    for spec in [x for x in os.environ.get("PROBE_BLOCKS", "2048,8192,16384,-4,-8,-16").split(",") if x and x != "none"]:
         # "<blocks>@<misalign>": the same probe over a base address misaligned by that many bytes
         blocks, mis = (int(x) for x in spec.split("@")) if "@" in spec else (int(spec), 0)
         ts = [probe(buf.data_ptr() + mis, buf.numel() - 64, sink.data_ptr(), blocks, st) for _ in range(6)][1:]

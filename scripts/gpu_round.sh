@@ -5,7 +5,7 @@ export TMPDIR=/tmp
 T=${TAG:-round}
 mkdir -p gpurun_out/$T
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/$T/smoke.log 2>&1 && \
-timeout -k 10 600 python -m pytest tests -q -m gpu > gpurun_out/$T/pytest_gpu.log 2>&1 && \
+timeout -k 10 600 python -u -m pytest tests -x -q -m gpu --timeout 120 --timeout-method thread > gpurun_out/$T/pytest_gpu.log 2>&1 && \
 timeout -k 10 400 python bench.py > gpurun_out/$T/bench.json 2> gpurun_out/$T/bench.err && \
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/$T/trace -o run -- \
     python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-extra > gpurun_out/$T/trace_bench.json 2> gpurun_out/$T/trace_bench.err && \

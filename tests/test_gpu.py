@@ -252,6 +252,24 @@ def test_tool_gpu_engine_matches_reference(tmp_path, datafile_cases, name):
     assert code == {c["name"]: c for c in datafile_cases}[name]["exit"]
 
 
+@pytest.mark.parametrize("jobs", [1, 3])
+def test_tool_gpu_multi_file_scan(tmp_path, datafile_cases, jobs):
+    """several datafiles in one run, worker threads sharing the GPU: every
+    report identical to the reference run on that file (tests/test_tool_multi.py)"""
+    from test_tool_multi import MULTI, check_multi
+    check_multi(MULTI, tmp_path, "hip", datafile_cases, [f"--jobs={jobs}"])
+
+
+def test_tool_gpu_multi_file_fatal(tmp_path):
+    from test_tool_cpu import expected
+    from test_tool_multi import run_multi
+    names = ["mixed", "corrupt_crc", "truncated_payload", "multi_errors", "zipf_small"]
+    out, err, code = run_multi(names, tmp_path, "hip", ["--jobs=4"])
+    assert out == "".join(expected(n)[0] for n in names[:3])
+    assert err == "".join(expected(n)[1] for n in names[:3])
+    assert code == 1
+
+
 # ------------------------------------------------------------------ C4 -------
 
 def test_c4_device_image_and_verify(dev, oracle_c):
