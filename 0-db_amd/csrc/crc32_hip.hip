@@ -61,8 +61,17 @@ constexpr uint32_t UNIT_OVH = 384;
 constexpr uint64_t MIN_UNITS_PER_WAVE = 256;
 // dword offsets inside the per-stream scratch: [0, 16384) one dummy store
 // word per wave, [16384, 131072) diagnostic stamps, [131072, 132096) per-CU
-// arrival counters (PRIO >= 2)
+// arrival counters (PRIO >= 2), [132096, 136192) tail-pool chunk counters
+// (DYN: 2 launch parities x up to 64 pools, one 128-byte line each)
 constexpr uint32_t SCRATCH_CU_CTR = 131072;
+constexpr uint32_t SCRATCH_DYN_CTR = 132096;
+constexpr uint32_t DYN_MAX_POOLS = 64;
+// the tail pool is used only when every slice holds at least this many units
+// (so every wave reaches the pool, and every pool has waves to drain it)
+constexpr uint64_t DYN_MIN_UNITS_PER_WAVE = 4096;
+// ... and no record spans more than this many chunks (each chunk cut of a
+// record is one same-address atomic XOR: one huge record would serialise them)
+constexpr uint64_t DYN_MAX_CHUNKS_PER_RECORD = 64;
 
 static_assert(ZDBCRC_LDS_DW % 4 == 0, "LDS image must be 16-byte granular");
 static_assert(ZDBCRC_LDS_DW * 4 * WG_PER_CU <= 160 * 1024, "LDS budget");
@@ -343,7 +352,17 @@ struct PlanArgs {
     const uint64_t *bsum;  // nb block totals (nullptr: local is global)
     uint32_t nb;
     uint32_t lg;
+    const uint32_t *bmax; // nb block maxima of a record's unit count (tail-pool guard)
 };
+
+__device__ __forceinline__ uint32_t wave_max(uint32_t x) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const uint32_t y = (uint32_t)__shfl_xor((int)x, o, 64);
+        x = y > x ? y : x;
+    }
+    return x;
+}
 
 // record r with unit_start[r] <= b < unit_start[r+1]: 64-way search, one
 // vector load per round (3 rounds for 1e5 records, 4 for 1e6)
@@ -518,8 +537,14 @@ __device__ __forceinline__ uint64_t block_excl_scan64(uint64_t v, uint64_t *wsum
 // NOZ: timing diagnostic only (skips the trailing-pad shift: wrong checksums)
 // NTL: payload loads carry the nontemporal hint (read once, never reused)
 // NOLOAD: timing diagnostic only (no payload loads: the compute floor; wrong checksums)
+// DYN > 0: tail pool.  Static slices cover the first (16 - DYN)/16 of the unit
+// space; the rest is split into DYN_POOLS pools (pool = blockIdx mod DYN_POOLS) of
+// CPW chunks per wave, claimed with one atomicAdd each as waves run out of
+// work, so waves that the arbitration favours take more of the tail and the
+// launch does not end on its slowest waves.  Cut partials of finished ranges
+// are flushed with atomic XOR at each claim (at most 2 are pending then).
 template <int WGT, int WPE, bool STAMP = false, int PRIO = 0, uint32_t UO = UNIT_OVH, bool NOZ = false,
-          bool NTL = false, bool NOLOAD = false, int XM = 0>
+          bool NTL = false, bool NOLOAD = false, int XM = 0, int DYN = 0, int CPW = 4, uint32_t DYN_POOLS = 8>
 __global__ __launch_bounds__(WGT, WPE) void crc_batch_kernel_v3(
     const uint8_t *__restrict__ arena, const uint64_t *__restrict__ offsets,
     const uint32_t *__restrict__ lengths, const PlanArgs plan, uint64_t n,
@@ -529,6 +554,7 @@ __global__ __launch_bounds__(WGT, WPE) void crc_batch_kernel_v3(
     __shared__ __attribute__((aligned(16))) uint32_t lds[ZDBCRC_LDS_DW + 16 + 2 * NSLOT];
     __shared__ uint64_t boff[PLAN_MAX_BLOCKS + 1];
     __shared__ uint64_t wsum[2 * NW + 1];
+    __shared__ uint32_t wmax[NW];
     uint32_t *const prog = lds + ZDBCRC_LDS_DW;   // per-wave progress (PRIO)
     uint32_t *const slot = prog + 16;             // cut records of the workgroup: [NSLOT] r, [NSLOT] x
     const uint64_t t_start = STAMP ? __builtin_amdgcn_s_memrealtime() : 0;
@@ -538,11 +564,21 @@ __global__ __launch_bounds__(WGT, WPE) void crc_batch_kernel_v3(
     if (plan.bsum) {
         constexpr uint32_t PER = (PLAN_MAX_BLOCKS + WGT - 1) / WGT;
         uint64_t v[PER], t = 0;
+        uint32_t mx = 0;
 #pragma unroll
         for (uint32_t i = 0; i < PER; i++) {
             const uint32_t b = threadIdx.x * PER + i;
             v[i] = b < plan.nb ? plan.bsum[b] : 0;
             t += v[i];
+            if (DYN) {
+                const uint32_t q = b < plan.nb ? plan.bmax[b] : 0u;
+                mx = q > mx ? q : mx;
+            }
+        }
+        if (DYN) {
+            mx = wave_max(mx);
+            if ((threadIdx.x & 63u) == 0)
+                wmax[threadIdx.x >> 6] = mx;
         }
         uint64_t total;
         uint64_t e = block_excl_scan64<WGT>(t, wsum, &total);
@@ -566,10 +602,21 @@ __global__ __launch_bounds__(WGT, WPE) void crc_batch_kernel_v3(
     uint64_t nwaves = (total + MIN_UNITS_PER_WAVE - 1) / MIN_UNITS_PER_WAVE;
     if (nwaves > max_waves)
         nwaves = max_waves;
-    const uint64_t ub = total * gw / nwaves;
-    const uint64_t ue = total * (gw + 1) / nwaves;
+    // tail pool only with a full grid whose slices are all long enough
+    bool dyn = DYN > 0 && plan.bmax && gridDim.x >= DYN_POOLS && total >= DYN_MIN_UNITS_PER_WAVE * max_waves;
+    if (dyn) { // largest record vs chunk size (wmax written before the scan's barriers)
+        uint32_t mxu = 0;
+        for (uint32_t i = 0; i < NW; i++)
+            mxu = wmax[i] > mxu ? wmax[i] : mxu;
+        const uint64_t chunk = total * DYN / 16 / ((uint64_t)CPW * nwaves);
+        dyn = mxu <= DYN_MAX_CHUNKS_PER_RECORD * chunk;
+    }
+    const uint64_t Ts = dyn ? total - total * DYN / 16 : total;
+    uint64_t ub = Ts * gw / nwaves;
+    uint64_t ue = Ts * (gw + 1) / nwaves;
     bool active = gw < nwaves && ub < ue;
     MetaBatch m;
+    m.rb = ~0ull;
     uint64_t rn = 0;
     Seg cur, nx;
     uint4 bufc[K], bufn[K];
@@ -599,18 +646,61 @@ __global__ __launch_bounds__(WGT, WPE) void crc_batch_kernel_v3(
         for (int i = threadIdx.x; i < ZDBCRC_LDS_DW / 4; i += WGT)
             dst[i] = src[i];
     }
+    if (blockIdx.x == 0 && threadIdx.x < DYN_MAX_POOLS) // the next launch's counters (every variant)
+        scratch[SCRATCH_DYN_CTR + (((epoch + 1u) & 1u) * DYN_MAX_POOLS + threadIdx.x) * 32u] = 0u;
     __syncthreads();
-    if (!active)
-        return;
+
+    uint64_t cut_r[2] = {0, 0};
+    uint32_t cut_x[2] = {0, 0}, ncut = 0;
+    uint64_t pbase = 0; // units of earlier ranges (PRIO progress)
+    // tail pool of this workgroup: chunk c covers [P0 + PL c / nch, P0 + PL (c+1) / nch)
+    const uint32_t pool = blockIdx.x % DYN_POOLS;
+    const uint64_t Td = total - Ts;
+    const uint64_t P0 = Ts + Td * pool / DYN_POOLS;
+    const uint64_t PL = Ts + Td * (pool + 1) / DYN_POOLS - P0;
+    const uint64_t nch = (uint64_t)CPW * (nwaves / DYN_POOLS);
+    static_assert(DYN_POOLS <= DYN_MAX_POOLS, "tail-pool counters");
+    uint32_t *const ctr = scratch + SCRATCH_DYN_CTR + ((epoch & 1u) * DYN_MAX_POOLS + pool) * 32u;
+    // next range from the pool; false once the pool is drained
+    auto claim = [&](Seg &sg) -> bool {
+        if (lane == 0) {
+            if (ncut > 0)
+                atomicXor(out + cut_r[0], cut_x[0]);
+            if (ncut > 1)
+                atomicXor(out + cut_r[1], cut_x[1]);
+        }
+        ncut = 0;
+        for (;;) {
+            uint32_t c = 0;
+            if (lane == 0)
+                c = atomicAdd(ctr, 1u);
+            c = __builtin_amdgcn_readfirstlane(c);
+            if (c >= nch)
+                return false;
+            pbase += ue - ub;
+            ub = P0 + PL * c / nch;
+            ue = P0 + PL * (c + 1) / nch;
+            if (ue <= ub)
+                continue;
+            rn = find_record(unit_start, n, ub, lane);
+            if (rn < m.rb)
+                load_meta(m, rn, n, lane, unit_start, arena, offsets, lengths);
+            if (next_seg_batched<UO>(rn, n, ub, ue, lane, m, unit_start, arena, offsets, lengths, sg))
+                return true;
+        }
+    };
+    if (!active) {
+        if (!(DYN && dyn && claim(cur)))
+            return;
+        load_superstep_v3<NTL, NOLOAD>(cur.c, 0, lane, bufc);
+    }
     const uint32_t young = PRIO >= 2 ? __builtin_amdgcn_readfirstlane(prog[15]) : 0u;
 
     uint32_t *const dummy = scratch + gw;
-    uint64_t cut_r[2] = {0, 0};
-    uint32_t cut_x[2] = {0, 0}, ncut = 0;
     uint32_t css = 0, acc = 0, iter = 0;
     for (;;) {
         if (PRIO && (++iter & 1) == 0) {
-            const uint32_t mine = (uint32_t)(cur.us + cur.c.pa + 64u * K * css - ub);
+            const uint32_t mine = (uint32_t)(pbase + cur.us + cur.c.pa + 64u * K * css - ub);
             if (lane == 0)
                 prog[wid] = mine;
             const uint32_t other = lane < (uint32_t)(WGT / 64) ? prog[lane] : 0u;
@@ -652,7 +742,8 @@ __global__ __launch_bounds__(WGT, WPE) void crc_batch_kernel_v3(
         if (css + 1 < cur.S) {
             nx = cur;
             nss = css + 1;
-        } else if (!next_seg_batched<UO>(rn, n, ub, ue, lane, m, unit_start, arena, offsets, lengths, nx)) {
+        } else if (!next_seg_batched<UO>(rn, n, ub, ue, lane, m, unit_start, arena, offsets, lengths, nx) &&
+                   !(DYN && dyn && claim(nx))) {
             more = false;
             nx = cur;
             nss = css;
@@ -733,6 +824,7 @@ struct KernelVariant {
 
 // selectable with ZDBCRC_VARIANT=<index> (A/B measurement); 0 is the default
 const KernelVariant kVariants[] = {
+    {"v3_wg768_nt_dyn6c4p32", crc_batch_kernel_v3<768, 6, false, 0, UNIT_OVH, false, true, false, 0, 6, 4, 32>, 768},
     {"v3_wg768_prio_nt", crc_batch_kernel_v3<768, 6, false, 1, UNIT_OVH, false, true>, 768},
     {"v3_wg768_prio", crc_batch_kernel_v3<768, 6, false, 1>, 768},
     {"v3_wg768_nt", crc_batch_kernel_v3<768, 6, false, 0, UNIT_OVH, false, true>, 768},
@@ -751,6 +843,14 @@ const KernelVariant kVariants[] = {
     {"v3_wg768_prio3_nt", crc_batch_kernel_v3<768, 6, false, 3, UNIT_OVH, false, true>, 768},
     {"v3_wg768_prio2_nt_stamp", crc_batch_kernel_v3<768, 6, true, 2, UNIT_OVH, false, true>, 768},
     {"v3_wg768_prio3_nt_stamp", crc_batch_kernel_v3<768, 6, true, 3, UNIT_OVH, false, true>, 768},
+    {"v3_wg768_nt_dyn6c2p32", crc_batch_kernel_v3<768, 6, false, 0, UNIT_OVH, false, true, false, 0, 6, 2, 32>, 768},
+    {"v3_wg768_nt_dyn6c3p32", crc_batch_kernel_v3<768, 6, false, 0, UNIT_OVH, false, true, false, 0, 6, 3, 32>, 768},
+    {"v3_wg768_nt_dyn6c2p64", crc_batch_kernel_v3<768, 6, false, 0, UNIT_OVH, false, true, false, 0, 6, 2, 64>, 768},
+    {"v3_wg768_nt_dyn6c4p64", crc_batch_kernel_v3<768, 6, false, 0, UNIT_OVH, false, true, false, 0, 6, 4, 64>, 768},
+    {"v3_wg768_nt_dyn5c4p32", crc_batch_kernel_v3<768, 6, false, 0, UNIT_OVH, false, true, false, 0, 5, 4, 32>, 768},
+    {"v3_wg768_nt_dyn7c4p32", crc_batch_kernel_v3<768, 6, false, 0, UNIT_OVH, false, true, false, 0, 7, 4, 32>, 768},
+    {"v3_wg768_nt_dyn8c4p64", crc_batch_kernel_v3<768, 6, false, 0, UNIT_OVH, false, true, false, 0, 8, 4, 64>, 768},
+    {"v3_wg768_nt_dyn6c4p32_stamp", crc_batch_kernel_v3<768, 6, true, 0, UNIT_OVH, false, true, false, 0, 6, 4, 32>, 768},
 };
 
 constexpr int kNumVariants = (int)(sizeof(kVariants) / sizeof(kVariants[0]));
@@ -795,8 +895,11 @@ __global__ __launch_bounds__(PLAN_T) void plan_kernel(const uint8_t *__restrict_
                                                       const uint64_t *__restrict__ offsets,
                                                       const uint32_t *__restrict__ lengths, uint64_t n, uint64_t ovh,
                                                       uint32_t lg, uint64_t *__restrict__ local,
-                                                      uint64_t *__restrict__ bsum, uint32_t *__restrict__ out) {
+                                                      uint64_t *__restrict__ bsum, uint32_t *__restrict__ bmax,
+                                                      uint32_t *__restrict__ out) {
     __shared__ uint64_t wsum[2 * (PLAN_T / 64) + 1];
+    __shared__ uint32_t wmx[PLAN_T / 64];
+    uint32_t mx = 0;
     const uint32_t per = (1u << lg) / PLAN_T;
     const uint64_t r0 = ((uint64_t)blockIdx.x << lg) + (uint64_t)threadIdx.x * per;
     uint64_t s = 0;
@@ -810,11 +913,15 @@ __global__ __launch_bounds__(PLAN_T) void plan_kernel(const uint8_t *__restrict_
                 v += record_pieces(a, L);
             }
             s += v;
+            mx = v > mx ? (uint32_t)v : mx;
             out[r] = 0;
         }
     }
+    mx = wave_max(mx);
+    if ((threadIdx.x & 63u) == 0)
+        wmx[threadIdx.x >> 6] = mx;
     uint64_t total;
-    uint64_t e = block_excl_scan64<PLAN_T>(s, wsum, &total);
+    uint64_t e = block_excl_scan64<PLAN_T>(s, wsum, &total); // its barriers publish wmx
     for (uint32_t i = 0; i < per; i++) {
         const uint64_t r = r0 + i;
         if (r > n)
@@ -830,8 +937,13 @@ __global__ __launch_bounds__(PLAN_T) void plan_kernel(const uint8_t *__restrict_
             e += v;
         }
     }
-    if (threadIdx.x == 0)
+    if (threadIdx.x == 0) {
         bsum[blockIdx.x] = total;
+        uint32_t m = 0;
+        for (uint32_t i = 0; i < PLAN_T / 64; i++)
+            m = wmx[i] > m ? wmx[i] : m;
+        bmax[blockIdx.x] = m;
+    }
 }
 
 __global__ void verify_kernel(const uint32_t *__restrict__ out, const uint32_t *__restrict__ expected,
@@ -968,11 +1080,11 @@ __global__ void synth_kernel(uint8_t *__restrict__ buf, uint64_t len, uint64_t s
 struct Workspace {
     void *ptr = nullptr;
     size_t bytes = 0;
+    uint32_t launches = 0; // checksum launches on this workspace (DYN counter parity)
 };
 
 struct DeviceCtx {
     bool ready = false;
-    uint32_t epoch = 0; // launch counter (kernel argument; diagnostics only)
     int cus = 0;
     uint32_t *d_tables = nullptr;
     std::map<void *, Workspace> ws; // per stream
@@ -1053,9 +1165,10 @@ int enqueue_batch(DeviceCtx &c, const uint8_t *arena, const uint64_t *offsets, c
     auto al = [](size_t x) { return (x + 255) & ~size_t(255); };
     const size_t local_bytes = d_unit_start ? 0 : al((n + 1) * sizeof(uint64_t));
     const size_t bsum_bytes = d_unit_start ? 0 : al(nb * sizeof(uint64_t));
-    // dummy dword per wave (64 KiB) | diagnostic stamps (448 KiB) | spare
-    const size_t scratch_bytes = (64 + 448 + 4) * 1024;
-    const size_t need = scratch_bytes + local_bytes + bsum_bytes;
+    const size_t bmax_bytes = d_unit_start ? 0 : al(nb * sizeof(uint32_t));
+    // dummy dword per wave (64 KiB) | diagnostic stamps (448 KiB) | per-CU counters (4 KiB) | DYN counters (16 KiB)
+    const size_t scratch_bytes = (64 + 448 + 4 + 16) * 1024;
+    const size_t need = scratch_bytes + local_bytes + bsum_bytes + bmax_bytes;
     Workspace &w = c.ws[reinterpret_cast<void *>(st)];
     if (w.bytes < need) {
         if (w.ptr) {
@@ -1073,16 +1186,17 @@ int enqueue_batch(DeviceCtx &c, const uint8_t *arena, const uint64_t *offsets, c
     // scratch first: its offset must not move with n
     uint32_t *scratch = static_cast<uint32_t *>(w.ptr);
     g_last_scratch = scratch; // diagnostics only (single-threaded measurement scripts)
-    PlanArgs plan{d_unit_start, nullptr, 0, 0};
+    PlanArgs plan{d_unit_start, nullptr, 0, 0, nullptr};
     if (!d_unit_start) {
         uint8_t *base = static_cast<uint8_t *>(w.ptr) + scratch_bytes;
         uint64_t *local = reinterpret_cast<uint64_t *>(base);
         uint64_t *bsum = reinterpret_cast<uint64_t *>(base + local_bytes);
+        uint32_t *bmax = reinterpret_cast<uint32_t *>(base + local_bytes + bsum_bytes);
         hipLaunchKernelGGL(plan_kernel, dim3((uint32_t)nb), dim3(PLAN_T), 0, st, arena, offsets, lengths, n,
-                           (uint64_t)kv.unit_ovh, lg, local, bsum, out);
+                           (uint64_t)kv.unit_ovh, lg, local, bsum, bmax, out);
         if (hipGetLastError() != hipSuccess)
             return ZDB_CRC32_ELAUNCH;
-        plan = PlanArgs{local, bsum, (uint32_t)nb, lg};
+        plan = PlanArgs{local, bsum, (uint32_t)nb, lg, bmax};
     } else if (hipMemsetAsync(out, 0, n * sizeof(uint32_t), st) != hipSuccess) {
         return ZDB_CRC32_ELAUNCH;
     }
@@ -1104,7 +1218,7 @@ int enqueue_batch(DeviceCtx &c, const uint8_t *arena, const uint64_t *offsets, c
         hipEventRecord(e0, st);
     }
     hipLaunchKernelGGL(kv.fn, dim3(grid), dim3(kv.threads), 0, st, arena, offsets, lengths, plan, n,
-                       out, c.d_tables, max_waves, scratch, ++c.epoch);
+                       out, c.d_tables, max_waves, scratch, ++w.launches);
     if (hipGetLastError() != hipSuccess)
         return ZDB_CRC32_ELAUNCH;
     if (e1) {

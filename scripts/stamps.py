@@ -10,7 +10,7 @@ import torch, zdbcrc
 sv = zdbcrc._lib.zdbcrc_debug_set_variant; sv.restype = C.c_char_p; sv.argtypes = [C.c_int]
 rd = zdbcrc._lib.zdbcrc_debug_read_stamps; rd.restype = C.c_int; rd.argtypes = [C.c_void_p, C.c_size_t]
 vname = sys.argv[2] if len(sys.argv) > 2 else "v3_wg768_prio_nt_stamp"
-idx = [i for i in range(20) if sv(i) and sv(i).decode() == vname][0]
+idx = [i for i in range(64) if sv(i) and sv(i).decode() == vname][0]
 sv(idx)
 for label in sys.argv[1].split(","):
     wl, size = label, 4 << 30

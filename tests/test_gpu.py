@@ -236,6 +236,33 @@ def test_repeat_is_deterministic(dev):
         np.testing.assert_array_equal(gpu_batch(dev, arena, offs, lens), a)
 
 
+def _tail_pool_batch(seed: int, big: int):
+    """~450 MB batch, above the tail pool's size threshold (4096 units per
+    wave): 60k empty records first (their static slices hold no segment, so
+    those waves start in the pool), mixed sizes, one `big` record."""
+    rng = np.random.default_rng(seed)
+    lens = np.concatenate([np.zeros(60_000, np.int64), rng.integers(0, 256 << 10, 3000), [big],
+                           rng.integers(0, 5000, 20_000)])
+    gaps = rng.integers(0, 24, len(lens))
+    offs = np.zeros(len(lens), np.int64)
+    offs[1:] = np.cumsum(lens[:-1] + gaps[:-1])
+    offs += 5
+    arena = oracle.splitmix_bytes(int(offs[-1] + lens[-1]) + 16, seed)
+    return arena, offs, lens
+
+
+def test_tail_pool_batches(dev, oracle_c):
+    """The default kernel's tail pool (chunks claimed by atomic counters whose
+    launch parity alternates): A (largest record 768 KiB, pool on) and B (one
+    64 MiB record: more chunks than the guard allows per record, pool off),
+    launched alternately so each counter parity is reused, bit-exact every time."""
+    cases = [_tail_pool_batch(41, 768 << 10), _tail_pool_batch(42, 64 << 20)]
+    want = [oracle_c.batch(a, o, l) for a, o, l in cases]
+    for _ in range(2):
+        for (a, o, l), w in zip(cases, want):
+            np.testing.assert_array_equal(gpu_batch(dev, a, o, l), w)
+
+
 # ------------------------------------------------------ integrity tool ------
 
 TOOL_CASES = ["mixed", "zipf_small", "fixed_4k", "corrupt_payload", "corrupt_crc", "multi_errors",
