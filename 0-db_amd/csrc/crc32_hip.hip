@@ -843,12 +843,8 @@ const KernelVariant kVariants[] = {
     {"v3_wg768_prio3_nt", crc_batch_kernel_v3<768, 6, false, 3, UNIT_OVH, false, true>, 768},
     {"v3_wg768_prio2_nt_stamp", crc_batch_kernel_v3<768, 6, true, 2, UNIT_OVH, false, true>, 768},
     {"v3_wg768_prio3_nt_stamp", crc_batch_kernel_v3<768, 6, true, 3, UNIT_OVH, false, true>, 768},
-    {"v3_wg768_nt_dyn6c4p32_uo192", crc_batch_kernel_v3<768, 6, false, 0, 192, false, true, false, 0, 6, 4, 32>, 768, WG_PER_CU, 192},
-    {"v3_wg768_nt_dyn6c4p32_uo256", crc_batch_kernel_v3<768, 6, false, 0, 256, false, true, false, 0, 6, 4, 32>, 768, WG_PER_CU, 256},
-    {"v3_wg768_nt_dyn6c4p32_uo512", crc_batch_kernel_v3<768, 6, false, 0, 512, false, true, false, 0, 6, 4, 32>, 768, WG_PER_CU, 512},
-    {"v3_wg768_nt_dyn6c4p32_uo768", crc_batch_kernel_v3<768, 6, false, 0, 768, false, true, false, 0, 6, 4, 32>, 768, WG_PER_CU, 768},
     {"v3_wg768_nt_dyn8c3p32", crc_batch_kernel_v3<768, 6, false, 0, UNIT_OVH, false, true, false, 0, 8, 3, 32>, 768},
-    {"v3_wg768_nt_dyn7c3p32", crc_batch_kernel_v3<768, 6, false, 0, UNIT_OVH, false, true, false, 0, 7, 3, 32>, 768},
+    {"v3_wg768_nt_dyn6c4p32_uo768", crc_batch_kernel_v3<768, 6, false, 0, 768, false, true, false, 0, 6, 4, 32>, 768, WG_PER_CU, 768},
     {"v3_wg768_nt_dyn6c4p32_stamp", crc_batch_kernel_v3<768, 6, true, 0, UNIT_OVH, false, true, false, 0, 6, 4, 32>, 768},
     {"v3_wg768_nt_dyn6c4p32_noload", crc_batch_kernel_v3<768, 6, false, 0, UNIT_OVH, false, true, true, 0, 6, 4, 32>, 768},
 };
