@@ -1213,10 +1213,14 @@ int enqueue_batch(DeviceCtx &c, const uint8_t *arena, const uint64_t *offsets, c
         }
         hipEventRecord(e0, st);
     }
+    // the launch counter picks the tail-pool counter parity; it advances only
+    // when a kernel was enqueued (each launch clears the next parity's counters)
+    const uint32_t ep = w.launches + 1;
     hipLaunchKernelGGL(kv.fn, dim3(grid), dim3(kv.threads), 0, st, arena, offsets, lengths, plan, n,
-                       out, c.d_tables, max_waves, scratch, ++w.launches);
+                       out, c.d_tables, max_waves, scratch, ep);
     if (hipGetLastError() != hipSuccess)
         return ZDB_CRC32_ELAUNCH;
+    w.launches = ep;
     if (e1) {
         hipEventRecord(e1, st);
         g_pending.emplace_back(e0, e1);

@@ -132,10 +132,32 @@ def record_pieces(a: int, L: int) -> int:
     return nr if (L & 15) == 0 and (nr + 63) >> 6 < (na + 63) >> 6 else na
 
 
+def ranges(total: int, nwaves: int, max_units: int, max_waves: int, dyn: int = 0, cpw: int = 4,
+           pools: int = 8, dyn_min_units: int = 4096, max_chunks_per_record: int = 64) -> list:
+    """The unit ranges the kernel's waves walk: static slices of the first
+    (16 - dyn)/16 of [0, total), then the tail pool's chunks (pool p of
+    `pools`, cpw chunks per wave) when the guards of crc_batch_kernel_v3 let
+    the pool run.  Which wave claims a chunk does not change the result (cut
+    partials are XORed), so the model only needs the ranges."""
+    dyn_on = (dyn > 0 and total >= dyn_min_units * max_waves and
+              max_units <= max_chunks_per_record * (total * dyn // 16 // (cpw * nwaves)))
+    ts = total - total * dyn // 16 if dyn_on else total
+    out = [(ts * gw // nwaves, ts * (gw + 1) // nwaves) for gw in range(nwaves)]
+    if dyn_on:
+        td = total - ts
+        nch = cpw * (nwaves // pools)
+        for p in range(pools):
+            p0 = ts + td * p // pools
+            pl = ts + td * (p + 1) // pools - p0
+            out += [(p0 + pl * c // nch, p0 + pl * (c + 1) // nch) for c in range(nch)]
+    return [(ub, ue) for ub, ue in out if ub < ue]
+
+
 def batch(arena: np.ndarray, offsets, lengths, tab: np.ndarray, max_waves: int = 4096,
-          min_units: int = MIN_UNITS_PER_WAVE, base_addr: int = 0) -> np.ndarray:
+          min_units: int = MIN_UNITS_PER_WAVE, base_addr: int = 0, **pool) -> np.ndarray:
     """out[r] as crc_batch_kernel computes it.  base_addr is the (virtual)
-    address of arena[0]; pieces are aligned on absolute addresses."""
+    address of arena[0]; pieces are aligned on absolute addresses.  `pool`:
+    the tail-pool parameters of `ranges` (default: no pool)."""
     offsets = np.asarray(offsets, dtype=np.int64)
     lengths = np.asarray(lengths, dtype=np.int64)
     n = len(offsets)
@@ -155,11 +177,7 @@ def batch(arena: np.ndarray, offsets, lengths, tab: np.ndarray, max_waves: int =
     unit_start[1:] = np.cumsum(units)
     total = int(unit_start[n])
     nwaves = min(max_waves, (total + min_units - 1) // min_units)
-    for gw in range(nwaves):
-        ub = total * gw // nwaves
-        ue = total * (gw + 1) // nwaves
-        if ub >= ue:
-            continue
+    for ub, ue in ranges(total, nwaves, int(units.max()), max_waves, **pool):
         r = int(np.searchsorted(unit_start, ub, side="right") - 1)
         while True:
             us = int(unit_start[r]) + UNIT_OVH

@@ -97,3 +97,30 @@ def test_record_relative_grid(oracle_c, tab):
     for mw, mu in ((4096, 256), (7, 1)):
         got = km.batch(arena, offs, lens, tab, max_waves=mw, min_units=mu)
         np.testing.assert_array_equal(got, oracle_c.batch(arena, offs, lens))
+
+
+@pytest.mark.parametrize("dyn,cpw,pools", [(6, 4, 4), (8, 3, 2), (16, 1, 1), (2, 5, 4)])
+def test_tail_pool_ranges(oracle_c, tab, dyn, cpw, pools):
+    """The tail pool (crc_batch_kernel_v3 DYN): static slices + pool chunks
+    tile the unit space exactly once, and the checksums match the oracle."""
+    arena, offs, lens = _case(100 + dyn, 40, 3000, 60_000)
+    units = np.array([km.record_pieces(3 + int(o), int(l)) if l else 0 for o, l in zip(offs, lens)]) + km.UNIT_OVH
+    total = int(units.sum())
+    rs = km.ranges(total, 16, int(units.max()), 16, dyn=dyn, cpw=cpw, pools=pools, dyn_min_units=8,
+                   max_chunks_per_record=1 << 30)
+    assert len(rs) > 16 or dyn == 16  # the pool ran (dyn 16: all of it)
+    edges = sorted(rs)
+    assert edges[0][0] == 0 and edges[-1][1] == total
+    assert all(a[1] == b[0] for a, b in zip(edges, edges[1:]))
+    got = km.batch(arena, offs, lens, tab, max_waves=16, min_units=1, base_addr=3, dyn=dyn, cpw=cpw,
+                   pools=pools, dyn_min_units=8, max_chunks_per_record=1 << 30)
+    np.testing.assert_array_equal(got, oracle_c.batch(arena, offs, lens))
+
+
+def test_tail_pool_guard():
+    """No pool below 4096 units per wave, or when one record would span more
+    than 64 chunks (its cut partials would serialise on one atomic)."""
+    assert len(km.ranges(4096 * 16 - 1, 16, 100, 16, dyn=6)) == 16
+    assert len(km.ranges(10 ** 7, 16, 100, 16, dyn=6, pools=8)) > 16
+    chunk = 10 ** 7 * 6 // 16 // (4 * 16)
+    assert len(km.ranges(10 ** 7, 16, 64 * chunk + 1, 16, dyn=6, pools=8)) == 16
