@@ -544,7 +544,8 @@ __device__ __forceinline__ uint64_t block_excl_scan64(uint64_t v, uint64_t *wsum
 // launch does not end on its slowest waves.  Cut partials of finished ranges
 // are flushed with atomic XOR at each claim (at most 2 are pending then).
 template <int WGT, int WPE, bool STAMP = false, int PRIO = 0, uint32_t UO = UNIT_OVH, bool NOZ = false,
-          bool NTL = false, bool NOLOAD = false, int XM = 0, int DYN = 0, int CPW = 4, uint32_t DYN_POOLS = 8>
+          bool NTL = false, bool NOLOAD = false, int XM = 0, int DYN = 0, int CPW = 4, uint32_t DYN_POOLS = 8,
+          bool SP = false>
 __global__ __launch_bounds__(WGT, WPE) void crc_batch_kernel_v3(
     const uint8_t *__restrict__ arena, const uint64_t *__restrict__ offsets,
     const uint32_t *__restrict__ lengths, const PlanArgs plan, uint64_t n,
@@ -663,6 +664,9 @@ __global__ __launch_bounds__(WGT, WPE) void crc_batch_kernel_v3(
     uint32_t *const ctr = scratch + SCRATCH_DYN_CTR + ((epoch & 1u) * DYN_MAX_POOLS + pool) * 32u;
     // next range from the pool; false once the pool is drained
     auto claim = [&](Seg &sg) -> bool {
+        if (SP) // SP: waves still in their static slice issue ahead of pool waves
+                // (C3 -1 to -2 %, profiles/r1/ab_dyn_sp*.jsonl)
+            __builtin_amdgcn_s_setprio(0);
         if (lane == 0) {
             if (ncut > 0)
                 atomicXor(out + cut_r[0], cut_x[0]);
@@ -689,6 +693,8 @@ __global__ __launch_bounds__(WGT, WPE) void crc_batch_kernel_v3(
                 return true;
         }
     };
+    if (SP && dyn)
+        __builtin_amdgcn_s_setprio(2);
     if (!active) {
         if (!(DYN && dyn && claim(cur)))
             return;
@@ -824,6 +830,7 @@ struct KernelVariant {
 
 // selectable with ZDBCRC_VARIANT=<index> (A/B measurement); 0 is the default
 const KernelVariant kVariants[] = {
+    {"v3_wg768_nt_dyn4c4p32_sp", crc_batch_kernel_v3<768, 6, false, 0, UNIT_OVH, false, true, false, 0, 4, 4, 32, true>, 768},
     {"v3_wg768_nt_dyn6c4p32", crc_batch_kernel_v3<768, 6, false, 0, UNIT_OVH, false, true, false, 0, 6, 4, 32>, 768},
     {"v3_wg768_prio_nt", crc_batch_kernel_v3<768, 6, false, 1, UNIT_OVH, false, true>, 768},
     {"v3_wg768_prio", crc_batch_kernel_v3<768, 6, false, 1>, 768},
@@ -845,8 +852,9 @@ const KernelVariant kVariants[] = {
     {"v3_wg768_prio3_nt_stamp", crc_batch_kernel_v3<768, 6, true, 3, UNIT_OVH, false, true>, 768},
     {"v3_wg768_nt_dyn8c3p32", crc_batch_kernel_v3<768, 6, false, 0, UNIT_OVH, false, true, false, 0, 8, 3, 32>, 768},
     {"v3_wg768_nt_dyn6c4p32_uo768", crc_batch_kernel_v3<768, 6, false, 0, 768, false, true, false, 0, 6, 4, 32>, 768, WG_PER_CU, 768},
-    {"v3_wg768_nt_dyn6c4p32_stamp", crc_batch_kernel_v3<768, 6, true, 0, UNIT_OVH, false, true, false, 0, 6, 4, 32>, 768},
-    {"v3_wg768_nt_dyn6c4p32_noload", crc_batch_kernel_v3<768, 6, false, 0, UNIT_OVH, false, true, true, 0, 6, 4, 32>, 768},
+    {"v3_wg768_nt_dyn4c4p32", crc_batch_kernel_v3<768, 6, false, 0, UNIT_OVH, false, true, false, 0, 4, 4, 32>, 768},
+    {"v3_wg768_nt_dyn4c4p32_sp_stamp", crc_batch_kernel_v3<768, 6, true, 0, UNIT_OVH, false, true, false, 0, 4, 4, 32, true>, 768},
+    {"v3_wg768_nt_dyn4c4p32_sp_noload", crc_batch_kernel_v3<768, 6, false, 0, UNIT_OVH, false, true, true, 0, 4, 4, 32, true>, 768},
 };
 
 constexpr int kNumVariants = (int)(sizeof(kVariants) / sizeof(kVariants[0]));

@@ -253,10 +253,10 @@ def _tail_pool_batch(seed: int, big: int):
 
 def test_tail_pool_batches(dev, oracle_c):
     """The default kernel's tail pool (chunks claimed by atomic counters whose
-    launch parity alternates): A (largest record 768 KiB, pool on) and B (one
+    launch parity alternates): A (largest record 512 KiB, pool on: < 64 chunks of ≈ 600 units) and B (one
     64 MiB record: more chunks than the guard allows per record, pool off),
     launched alternately so each counter parity is reused, bit-exact every time."""
-    cases = [_tail_pool_batch(41, 768 << 10), _tail_pool_batch(42, 64 << 20)]
+    cases = [_tail_pool_batch(41, 512 << 10), _tail_pool_batch(42, 64 << 20)]
     want = [oracle_c.batch(a, o, l) for a, o, l in cases]
     for _ in range(2):
         for (a, o, l), w in zip(cases, want):
