@@ -46,6 +46,7 @@
 
 #include "crc32c_gf2.h"
 #include "zdb_crc32.h"
+#include "zdb_datafile.h"
 
 namespace {
 
@@ -961,6 +962,51 @@ __global__ void verify_kernel(const uint32_t *__restrict__ out, const uint32_t *
     }
 }
 
+// batched CHECK, phase 1: decode the entry header at each index-given offset
+// (data_entry_header_t, data.h:56-65: u8 idlength, u32 datalength, u32
+// previous, u32 integrity, ...; 18 bytes, packed LE) into checksum
+// descriptors.  Records whose header or payload leaves the image get length 0
+// and status -1 (data_check_real's short reads, data.c:540-555).
+__device__ __forceinline__ uint32_t le32_at(const uint8_t *p) {
+    return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
+}
+
+__global__ void check_decode_kernel(const uint8_t *__restrict__ image, uint64_t image_len,
+                                    const uint64_t *__restrict__ rec_off, uint64_t n,
+                                    uint64_t *__restrict__ offs, uint32_t *__restrict__ lens,
+                                    uint32_t *__restrict__ expect, int32_t *__restrict__ result) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n)
+        return;
+    const uint64_t o = rec_off[i];
+    uint64_t po = 0;
+    uint32_t len = 0, crc = 0;
+    int32_t st = -1;
+    if (o <= image_len && image_len - o >= ZDB_ENTRY_HEADER_SIZE) {
+        const uint8_t *h = image + o;
+        const uint64_t p = o + ZDB_ENTRY_HEADER_SIZE + h[0];
+        const uint32_t L = le32_at(h + 1);
+        if (p <= image_len && image_len - p >= L) {
+            po = p;
+            len = L;
+            crc = le32_at(h + 9);
+            st = 0;
+        }
+    }
+    offs[i] = po;
+    lens[i] = len;
+    expect[i] = crc;
+    result[i] = st;
+}
+
+// phase 2: 1 / 0 from the computed checksums, -1 kept
+__global__ void check_finish_kernel(const uint32_t *__restrict__ out, const uint32_t *__restrict__ expect,
+                                    uint64_t n, int32_t *__restrict__ result) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n && result[i] == 0)
+        result[i] = out[i] == expect[i] ? 1 : 0;
+}
+
 // read-only streaming probe (measurement aid): XOR of every 16-byte word,
 // one dword written per workgroup -- the achievable HBM read ceiling the
 // checksum kernel is compared with
@@ -1398,6 +1444,44 @@ int zdb_crc32_verify_device(const uint8_t *d_arena, const uint64_t *d_offsets, c
     hipLaunchKernelGGL(verify_kernel, dim3(blocks), dim3(256), 0, st, d_out, d_expected, (uint64_t)n,
                        d_mismatch, d_mismatch_count, max_mismatch);
     return hipGetLastError() == hipSuccess ? ZDB_CRC32_OK : ZDB_CRC32_ELAUNCH;
+}
+
+int zdb_datafile_check_device(const uint8_t *d_image, uint64_t image_len, const uint64_t *d_offsets,
+                              int32_t *d_result, size_t n, void *stream) {
+    if (n == 0)
+        return ZDB_CRC32_OK;
+    if (!d_image || !d_offsets || !d_result)
+        return ZDB_CRC32_EINVAL;
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    int dev;
+    int rc = current_device(&dev);
+    if (rc)
+        return rc;
+    std::lock_guard<std::mutex> g(g_dev_mu[dev]);
+    DeviceCtx *c;
+    if ((rc = ensure_device(dev, &c)))
+        return rc;
+    // descriptors: offsets (8 B) | lengths, expected, out (4 B each) per record
+    void *tmp = nullptr;
+    if (hipMallocAsync(&tmp, n * 20, st) != hipSuccess)
+        return ZDB_CRC32_ENOMEM;
+    uint64_t *offs = static_cast<uint64_t *>(tmp);
+    uint32_t *lens = reinterpret_cast<uint32_t *>(offs + n);
+    uint32_t *expect = lens + n;
+    uint32_t *out = expect + n;
+    const uint32_t blocks = (uint32_t)((n + 255) / 256);
+    hipLaunchKernelGGL(check_decode_kernel, dim3(blocks), dim3(256), 0, st, d_image, image_len, d_offsets,
+                       (uint64_t)n, offs, lens, expect, d_result);
+    rc = hipGetLastError() == hipSuccess ? ZDB_CRC32_OK : ZDB_CRC32_ELAUNCH;
+    if (!rc)
+        rc = enqueue_batch(*c, d_image, offs, lens, out, n, st);
+    if (!rc) {
+        hipLaunchKernelGGL(check_finish_kernel, dim3(blocks), dim3(256), 0, st, out, expect, (uint64_t)n,
+                           d_result);
+        rc = hipGetLastError() == hipSuccess ? ZDB_CRC32_OK : ZDB_CRC32_ELAUNCH;
+    }
+    hipFreeAsync(tmp, st);
+    return rc;
 }
 
 int zdb_crc32_batch(const uint8_t *arena, size_t arena_len, const uint64_t *offsets, const uint32_t *lengths,

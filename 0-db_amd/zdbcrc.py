@@ -66,6 +66,7 @@ _batch_device = _fn("zdb_crc32_batch_device", C.c_int, vp, vp, vp, vp, C.c_size_
 _verify_device = _fn("zdb_crc32_verify_device", C.c_int, vp, vp, vp, vp, vp, vp, vp, C.c_uint32,
                      C.c_size_t, vp)
 _batch_host = _fn("zdb_crc32_batch", C.c_int, vp, C.c_size_t, vp, vp, vp, C.c_size_t)
+_check_device = _fn("zdb_datafile_check_device", C.c_int, vp, C.c_uint64, vp, vp, C.c_size_t, vp)
 _host_alloc = _fn("zdb_crc32_host_alloc", vp, C.c_size_t)
 _host_free = _fn("zdb_crc32_host_free", None, vp)
 _set_timing = _fn("zdb_crc32_set_timing", None, C.c_int)
@@ -93,7 +94,7 @@ EXPORTED = [
     "zdb_crc32_host_free", "zdb_crc32_set_timing",
     "zdb_crc32_kernel_stats", "zdb_synth_fill", "zdb_synth_fill_device", "zdb_synth_zipf_lengths",
     "zdb_datafile_walk", "zdb_datafile_encode_entry", "zdb_datafile_encode_header",
-    "zdb_datafile_payloads", "zdb_datafile_encode_batch",
+    "zdb_datafile_payloads", "zdb_datafile_encode_batch", "zdb_datafile_check_device",
 ]
 
 RECORD_DTYPE = np.dtype([
@@ -198,6 +199,17 @@ def batch_device(arena, offsets, lengths, out, stream=None):
     _check(_batch_device(arena.data_ptr(), offsets.data_ptr(), lengths.data_ptr(), out.data_ptr(), n,
                          _stream_handle(stream)), "zdb_crc32_batch_device")
     return out
+
+
+def datafile_check_device(image, record_offsets, result, stream=None):
+    """Batched CHECK (data_check_real, data.c:533-571) over a device-resident
+    datafile image: result[i] = 1 / 0 / -1 (match / mismatch / short read)."""
+    import torch
+    for t, d, nm in ((image, torch.uint8, "image"), (record_offsets, torch.int64, "record_offsets"),
+                     (result, torch.int32, "result")):
+        _dev_check(t, d, nm)
+    _check(_check_device(image.data_ptr(), image.numel(), record_offsets.data_ptr(), result.data_ptr(),
+                         record_offsets.numel(), _stream_handle(stream)), "zdb_datafile_check_device")
 
 
 def verify_device(arena, offsets, lengths, expected, out, mismatch, count, stream=None):

@@ -84,6 +84,18 @@ size_t zdb_datafile_encode_batch(uint8_t *dst, size_t cap, uint64_t file_offset,
 size_t zdb_datafile_payloads(const zdb_record_t *recs, size_t nrecs, uint64_t *offsets, uint32_t *lengths,
                              uint32_t *expected, uint32_t *record_index);
 
+/* Batched CHECK (f4): data_check_real (data.c:533-571, the CHECK command,
+ * commands_dataset.c:54-102) for n index-given record offsets at once, over a
+ * datafile image resident in device memory (d_image[0..image_len)).  For
+ * record i: decode the entry header at d_offsets[i], checksum its payload on
+ * the GPU and compare with the header's integrity field.  d_result[i] (device
+ * i32) = 1 when they match, 0 when not, -1 when the header or the payload
+ * does not fit in the image (the reference's short-read -1).  Enqueued on
+ * `stream` (a hipStream_t, NULL = default); HIP errors are returned, there
+ * is no CPU fallback. */
+int zdb_datafile_check_device(const uint8_t *d_image, uint64_t image_len, const uint64_t *d_offsets,
+                              int32_t *d_result, size_t n, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

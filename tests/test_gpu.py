@@ -344,3 +344,37 @@ def test_full_size_c4_shard_digest(dev, digests):
     assert int(cnt.item()) == 0
     del img
     torch.cuda.empty_cache()
+
+
+def _check_real(img: np.ndarray, off: int, crc32) -> int:
+    """data_check_real (data.c:533-571) on an in-memory image: -1 on a short
+    header or payload read, else payload crc == header integrity."""
+    if off + 18 > len(img):
+        return -1
+    idlen = int(img[off])
+    dlen = int(img[off + 1:off + 5].view("<u4")[0])
+    integ = int(img[off + 9:off + 13].view("<u4")[0])
+    p = off + 18 + idlen
+    if p + dlen > len(img):
+        return -1
+    return int(crc32(img[p:p + dlen]) == integ)
+
+
+@pytest.mark.parametrize("name", ["mixed", "zipf_small", "fixed_4k", "corrupt_payload", "corrupt_crc",
+                                  "multi_errors", "truncated_payload"])
+def test_batched_check_device(dev, oracle_c, name):
+    """f4: batched CHECK over a reference-written datafile image in HBM, one
+    launch for every record the index would point at, plus offsets whose
+    header or payload leaves the image (-1) and the file header itself."""
+    img = np.fromfile(GOLDEN / "datafiles" / f"{name}.d0", dtype=np.uint8)
+    recs, _ = dev.datafile_walk(img)
+    offs = [int(o) for o in recs["header_offset"]] + [0, 28, len(img) - 5, len(img) - 18, len(img) + 100]
+    want = np.array([_check_real(img, o, oracle_c.crc32) for o in offs], np.int32)
+    d_img = torch.from_numpy(img.copy()).cuda()
+    d_off = torch.tensor(offs, dtype=torch.int64, device="cuda")
+    res = torch.full((len(offs),), 7, dtype=torch.int32, device="cuda")
+    dev.datafile_check_device(d_img, d_off, res)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(res.cpu().numpy(), want)
+    if name.startswith("corrupt") or name == "multi_errors":
+        assert (want[:len(recs)] == 0).any()
