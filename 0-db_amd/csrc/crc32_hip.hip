@@ -42,6 +42,7 @@
 #include <mutex>
 #include <vector>
 
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
 #include "crc32c_gf2.h"
@@ -1265,20 +1266,23 @@ int enqueue_batch(DeviceCtx &c, const uint8_t *arena, const uint64_t *offsets, c
                 hipEventCreate(e);
             }
         }
-        hipEventRecord(e0, st);
     }
     // the launch counter picks the tail-pool counter parity; it advances only
     // when a kernel was enqueued (each launch clears the next parity's counters)
     const uint32_t ep = w.launches + 1;
-    hipLaunchKernelGGL(kv.fn, dim3(grid), dim3(kv.threads), 0, st, arena, offsets, lengths, plan, n,
-                       out, c.d_tables, max_waves, scratch, ep);
+    // timing: the dispatch packet itself carries the start/stop events
+    // (hipExtLaunchKernel), so no marker packets sit between the kernels
+    if (e0)
+        hipExtLaunchKernelGGL(kv.fn, dim3(grid), dim3(kv.threads), 0, st, e0, e1, 0u, arena, offsets, lengths,
+                              plan, n, out, c.d_tables, max_waves, scratch, ep);
+    else
+        hipLaunchKernelGGL(kv.fn, dim3(grid), dim3(kv.threads), 0, st, arena, offsets, lengths, plan, n,
+                           out, c.d_tables, max_waves, scratch, ep);
     if (hipGetLastError() != hipSuccess)
         return ZDB_CRC32_ELAUNCH;
     w.launches = ep;
-    if (e1) {
-        hipEventRecord(e1, st);
+    if (e1)
         g_pending.emplace_back(e0, e1);
-    }
     return ZDB_CRC32_OK;
 }
 
