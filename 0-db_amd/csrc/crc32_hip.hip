@@ -1209,7 +1209,7 @@ int enqueue_batch(DeviceCtx &c, const uint8_t *arena, const uint64_t *offsets, c
         return ZDB_CRC32_EINVAL;
     const KernelVariant &kv = variant();
     // planner blocks: 2^lg records each (n + 1 entries), at most PLAN_MAX_BLOCKS
-    uint32_t lg = 10;
+    uint32_t lg = 8; // one record per planner thread (PLAN_T = 256) until the block count limit
     while (((n + 1 + (1ull << lg) - 1) >> lg) > PLAN_MAX_BLOCKS)
         lg++;
     const uint64_t nb = (n + 1 + (1ull << lg) - 1) >> lg;
