@@ -181,3 +181,16 @@ def test_encode_batch_matches_reference_inserts():
     assert bytes(got) == img
     assert prev == int(recs["header_offset"][-1])
     np.testing.assert_array_equal(eo, recs["header_offset"])
+
+
+def test_check_device_argument_errors_without_gpu():
+    """zdb_datafile_check_device: an empty batch is a no-op and null device
+    pointers are rejected before HIP is touched (CPU-only: no compute call)."""
+    f = zdbcrc._check_device
+    assert f(None, 0, None, None, 0, None) == 0
+    assert f(None, 100, None, None, 5, None) == -2  # ZDB_CRC32_EINVAL (zdb_crc32.h)
+    code = ("import sys; sys.path.insert(0, %r); import zdbcrc; "
+            "zdbcrc._check_device(None, 0, None, None, 0, None); print(zdbcrc.gpu_initialized())"
+            % str(ROOT / "0-db_amd"))
+    out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, check=True)
+    assert out.stdout.split() == ["False"]
