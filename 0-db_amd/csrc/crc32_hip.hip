@@ -202,12 +202,14 @@ __device__ __forceinline__ uint32_t uniform_shift(uint32_t x, const uint32_t *__
     return r;
 }
 
+#ifdef ZDBCRC_DIAG
 __device__ __forceinline__ uint32_t wave_xor(uint32_t x) {
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1)
         x ^= __shfl_xor(x, o, 64);
     return x;
 }
+#endif
 
 // keep bytes [lo, hi) of dword k of a 16-byte piece (0 <= lo <= hi <= 16)
 __device__ __forceinline__ uint32_t keep_mask(int lo, int hi, int k) {
@@ -830,7 +832,10 @@ struct KernelVariant {
     uint32_t unit_ovh = UNIT_OVH; // must match the kernel's UO
 };
 
-// selectable with ZDBCRC_VARIANT=<index> (A/B measurement); 0 is the default
+#ifdef ZDBCRC_DIAG
+// diagnostic library only (libzdbcrc_diag.so, scripts/ab.py): A/B variants,
+// several of which compute wrong checksums by design (NOZ, NOLOAD, XM);
+// selectable with ZDBCRC_VARIANT=<index> or zdbcrc_debug_set_variant
 const KernelVariant kVariants[] = {
     {"v3_wg768_nt_dyn4c4p32_sp", crc_batch_kernel_v3<768, 6, false, 0, UNIT_OVH, false, true, false, 0, 4, 4, 32, true>, 768},
     {"v3_wg768_nt_dyn6c4p32", crc_batch_kernel_v3<768, 6, false, 0, UNIT_OVH, false, true, false, 0, 6, 4, 32>, 768},
@@ -858,18 +863,29 @@ const KernelVariant kVariants[] = {
     {"v3_wg768_nt_dyn4c4p32_sp_stamp", crc_batch_kernel_v3<768, 6, true, 0, UNIT_OVH, false, true, false, 0, 4, 4, 32, true>, 768},
     {"v3_wg768_nt_dyn4c4p32_sp_noload", crc_batch_kernel_v3<768, 6, false, 0, UNIT_OVH, false, true, true, 0, 4, 4, 32, true>, 768},
 };
-
 constexpr int kNumVariants = (int)(sizeof(kVariants) / sizeof(kVariants[0]));
-int g_variant = -1;
+std::atomic<int> g_variant{-1};
 
 const KernelVariant &variant() {
-    if (g_variant < 0) {
+    int v = g_variant.load();
+    if (v < 0) {
         const char *e = std::getenv("ZDBCRC_VARIANT");
-        int i = e ? std::atoi(e) : 0;
-        g_variant = (i >= 0 && i < kNumVariants) ? i : 0;
+        const int i = e ? std::atoi(e) : 0;
+        int expect = -1;
+        g_variant.compare_exchange_strong(expect, (i >= 0 && i < kNumVariants) ? i : 0);
+        v = g_variant.load();
     }
-    return kVariants[g_variant];
+    return kVariants[v];
 }
+#else
+// the product library ships exactly one checksum kernel: tail pool (4/16 of
+// the units, 32 pools, 4 chunks per wave) with static-phase priority, 768
+// threads, nontemporal payload loads; no environment knob
+const KernelVariant kDefault = {"v3_wg768_nt_dyn4c4p32_sp",
+                                crc_batch_kernel_v3<768, 6, false, 0, UNIT_OVH, false, true, false, 0, 4, 4, 32, true>,
+                                768};
+const KernelVariant &variant() { return kDefault; }
+#endif
 
 // unit count per record: ovh (the variant's per-record charge) + number of
 // 16-byte pieces it touches
@@ -987,8 +1003,11 @@ __global__ void check_decode_kernel(const uint8_t *__restrict__ image, uint64_t 
         const uint8_t *h = image + o;
         const uint64_t p = o + ZDB_ENTRY_HEADER_SIZE + h[0];
         const uint32_t L = le32_at(h + 1);
-        if (p <= image_len && image_len - p >= L) {
-            po = p;
+        // read(fd, buf, 0) succeeds wherever the file position is, so an
+        // empty payload is checked (crc 0 vs integrity) even when the key
+        // runs past the end of the image (data.c:546-551)
+        if (L == 0 || (p <= image_len && image_len - p >= L)) {
+            po = L ? p : 0;
             len = L;
             crc = le32_at(h + 9);
             st = 0;
@@ -1008,6 +1027,7 @@ __global__ void check_finish_kernel(const uint32_t *__restrict__ out, const uint
         result[i] = out[i] == expect[i] ? 1 : 0;
 }
 
+#ifdef ZDBCRC_DIAG
 // read-only streaming probe (measurement aid): XOR of every 16-byte word,
 // one dword written per workgroup -- the achievable HBM read ceiling the
 // checksum kernel is compared with
@@ -1104,6 +1124,8 @@ __global__ __launch_bounds__(768, 6) void lds_bench_kernel(uint32_t iters, uint3
         sink[0] = x;
 }
 
+#endif // ZDBCRC_DIAG
+
 __device__ __forceinline__ uint64_t mix64(uint64_t z) {
     z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
     z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
@@ -1141,20 +1163,29 @@ struct DeviceCtx {
     std::map<void *, Workspace> ws; // per stream
 };
 
+// a launch bracketed by timing events (created on device `dev`)
+struct TimedLaunch {
+    int dev;
+    hipEvent_t e0, e1;
+};
+
 // Locking: one mutex per device serialises that device's context,
 // workspaces and host staging (calls on different devices -- one host thread
 // per GPU in the multi-file scan -- run concurrently); g_mu guards the
-// process-wide measurement state (timing events, variant selection).
+// process-wide measurement state (pending timed launches, per-device event
+// pools, accumulated time).
 std::mutex g_mu;
 std::mutex g_dev_mu[64];
-uint32_t *g_last_scratch = nullptr;
 DeviceCtx g_dev[64];
 std::atomic<bool> g_hip_touched{false};
-bool g_timing = false;
-std::vector<std::pair<hipEvent_t, hipEvent_t>> g_pending;
+std::atomic<bool> g_timing{false};
+std::vector<TimedLaunch> g_pending;
 double g_time_ms = 0;
 uint64_t g_launches = 0;
-std::vector<hipEvent_t> g_event_pool;
+std::vector<hipEvent_t> g_event_pool[64]; // events are reused on the device they were created on
+#ifdef ZDBCRC_DIAG
+uint32_t *g_last_scratch = nullptr; // STAMP read-back (single-threaded measurement scripts)
+#endif
 
 std::vector<uint32_t> &host_tables() {
     static std::vector<uint32_t> t;
@@ -1203,11 +1234,11 @@ int ensure_device(int dev, DeviceCtx **out_ctx) {
 // enqueue plan + main kernel; caller holds the device's g_dev_mu
 // d_unit_start: the per-record unit prefix when the caller already has it
 // (host-planned batches); nullptr -> computed on the device by the scan
-int enqueue_batch(DeviceCtx &c, const uint8_t *arena, const uint64_t *offsets, const uint32_t *lengths,
-                  uint32_t *out, uint64_t n, hipStream_t st, const uint64_t *d_unit_start = nullptr) {
+int enqueue_batch(int dev, DeviceCtx &c, const KernelVariant &kv, const uint8_t *arena, const uint64_t *offsets,
+                  const uint32_t *lengths, uint32_t *out, uint64_t n, hipStream_t st,
+                  const uint64_t *d_unit_start = nullptr) {
     if (n > 0xFFFFFFFFull) // record indices are 32-bit on the device (cut lists, mismatch indices)
         return ZDB_CRC32_EINVAL;
-    const KernelVariant &kv = variant();
     // planner blocks: 2^lg records each (n + 1 entries), at most PLAN_MAX_BLOCKS
     uint32_t lg = 8; // one record per planner thread (PLAN_T = 256) until the block count limit
     while (((n + 1 + (1ull << lg) - 1) >> lg) > PLAN_MAX_BLOCKS)
@@ -1236,7 +1267,9 @@ int enqueue_batch(DeviceCtx &c, const uint8_t *arena, const uint64_t *offsets, c
     }
     // scratch first: its offset must not move with n
     uint32_t *scratch = static_cast<uint32_t *>(w.ptr);
-    g_last_scratch = scratch; // diagnostics only (single-threaded measurement scripts)
+#ifdef ZDBCRC_DIAG
+    g_last_scratch = scratch;
+#endif
     PlanArgs plan{d_unit_start, nullptr, 0, 0, nullptr};
     if (!d_unit_start) {
         uint8_t *base = static_cast<uint8_t *>(w.ptr) + scratch_bytes;
@@ -1256,15 +1289,22 @@ int enqueue_batch(DeviceCtx &c, const uint8_t *arena, const uint64_t *offsets, c
     const uint32_t max_waves = grid * (uint32_t)(kv.threads / 64);
     hipEvent_t e0 = nullptr, e1 = nullptr;
     std::unique_lock<std::mutex> tl(g_mu, std::defer_lock);
-    if (g_timing) {
+    if (g_timing.load()) {
         tl.lock();
+        std::vector<hipEvent_t> &pool = g_event_pool[dev];
         for (hipEvent_t *e : {&e0, &e1}) {
-            if (!g_event_pool.empty()) {
-                *e = g_event_pool.back();
-                g_event_pool.pop_back();
-            } else {
-                hipEventCreate(e);
+            if (!pool.empty()) {
+                *e = pool.back();
+                pool.pop_back();
+            } else if (hipEventCreate(e) != hipSuccess) {
+                *e = nullptr;
             }
+        }
+        if (!e0 || !e1) { // no timing for this launch rather than a half-bracketed one
+            for (hipEvent_t e : {e0, e1})
+                if (e)
+                    pool.push_back(e);
+            e0 = e1 = nullptr;
         }
     }
     // the launch counter picks the tail-pool counter parity; it advances only
@@ -1282,7 +1322,7 @@ int enqueue_batch(DeviceCtx &c, const uint8_t *arena, const uint64_t *offsets, c
         return ZDB_CRC32_ELAUNCH;
     w.launches = ep;
     if (e1)
-        g_pending.emplace_back(e0, e1);
+        g_pending.push_back(TimedLaunch{dev, e0, e1});
     return ZDB_CRC32_OK;
 }
 
@@ -1313,17 +1353,20 @@ const char *zdb_crc32_strerror(int code) {
     }
 }
 
+// the engine of the calling thread's current device; never initialises HIP
 const char *zdb_crc32_batch_engine(void) {
-    for (int d = 0; d < 64; d++) {
-        std::lock_guard<std::mutex> g(g_dev_mu[d]);
-        if (g_dev[d].ready)
-            return "hip-gfx950";
-    }
-    return "uninitialized";
+    if (!g_hip_touched.load())
+        return "uninitialized";
+    int dev = -1;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64)
+        return "uninitialized";
+    std::lock_guard<std::mutex> g(g_dev_mu[dev]);
+    return g_dev[dev].ready ? "hip-gfx950" : "uninitialized";
 }
 
 int zdb_crc32_gpu_initialized(void) { return g_hip_touched ? 1 : 0; }
 
+#ifdef ZDBCRC_DIAG
 // measurement hook (not part of the public ABI): time a read-only stream of
 // `bytes` (multiple of 16) with HIP events; returns ms, <0 on error
 float zdbcrc_debug_stream_read(const void *d_buf, size_t bytes, uint32_t *d_sink, int blocks, void *stream) {
@@ -1395,12 +1438,13 @@ int zdbcrc_debug_read_stamps(uint64_t *host, size_t waves) {
 // measurement hook (not part of the public ABI): select a kernel variant for
 // A/B timing in one process; returns its name, NULL if out of range
 const char *zdbcrc_debug_set_variant(int idx) {
-    std::lock_guard<std::mutex> g(g_mu);
     if (idx < 0 || idx >= kNumVariants)
         return nullptr;
     g_variant = idx;
     return kVariants[idx].name;
 }
+
+#endif // ZDBCRC_DIAG
 
 int zdb_crc32_batch_device(const uint8_t *d_arena, const uint64_t *d_offsets, const uint32_t *d_lengths,
                            uint32_t *d_out, size_t n, void *stream) {
@@ -1416,7 +1460,8 @@ int zdb_crc32_batch_device(const uint8_t *d_arena, const uint64_t *d_offsets, co
     DeviceCtx *c;
     if ((rc = ensure_device(dev, &c)))
         return rc;
-    return enqueue_batch(*c, d_arena, d_offsets, d_lengths, d_out, n, static_cast<hipStream_t>(stream));
+    return enqueue_batch(dev, *c, variant(), d_arena, d_offsets, d_lengths, d_out, n,
+                         static_cast<hipStream_t>(stream));
 }
 
 int zdb_crc32_verify_device(const uint8_t *d_arena, const uint64_t *d_offsets, const uint32_t *d_lengths,
@@ -1440,7 +1485,7 @@ int zdb_crc32_verify_device(const uint8_t *d_arena, const uint64_t *d_offsets, c
             return ZDB_CRC32_OK;
         if (!d_arena || !d_offsets || !d_lengths || !d_out)
             return ZDB_CRC32_EINVAL;
-        rc = enqueue_batch(*c, d_arena, d_offsets, d_lengths, d_out, n, st);
+        rc = enqueue_batch(dev, *c, variant(), d_arena, d_offsets, d_lengths, d_out, n, st);
         if (rc)
             return rc;
     }
@@ -1478,7 +1523,7 @@ int zdb_datafile_check_device(const uint8_t *d_image, uint64_t image_len, const 
                        (uint64_t)n, offs, lens, expect, d_result);
     rc = hipGetLastError() == hipSuccess ? ZDB_CRC32_OK : ZDB_CRC32_ELAUNCH;
     if (!rc)
-        rc = enqueue_batch(*c, d_image, offs, lens, out, n, st);
+        rc = enqueue_batch(dev, *c, variant(), d_image, offs, lens, out, n, st);
     if (!rc) {
         hipLaunchKernelGGL(check_finish_kernel, dim3(blocks), dim3(256), 0, st, out, expect, (uint64_t)n,
                            d_result);
@@ -1494,8 +1539,8 @@ int zdb_crc32_batch(const uint8_t *arena, size_t arena_len, const uint64_t *offs
         return ZDB_CRC32_OK;
     if (!arena || !offsets || !lengths || !out)
         return ZDB_CRC32_EINVAL;
-    for (size_t r = 0; r < n; r++)
-        if (offsets[r] + lengths[r] > arena_len)
+    for (size_t r = 0; r < n; r++) // overflow-safe: offsets[r] may be near UINT64_MAX
+        if (offsets[r] > arena_len || lengths[r] > arena_len - offsets[r])
             return ZDB_CRC32_EINVAL;
     int dev;
     int rc = current_device(&dev);
@@ -1541,7 +1586,8 @@ int zdb_crc32_batch(const uint8_t *arena, size_t arena_len, const uint64_t *offs
     uint32_t *hout = reinterpret_cast<uint32_t *>(h.hplan + n * 12 + (n + 1) * 8);
     std::memcpy(ho, offsets, n * 8);
     std::memcpy(hl, lengths, n * 4);
-    const UnitCount uc{h.arena, offsets, lengths, n, variant().unit_ovh};
+    const KernelVariant &kv = variant(); // resolved once: the host prefix and the kernel agree on UO
+    const UnitCount uc{h.arena, offsets, lengths, n, kv.unit_ovh};
     uint64_t acc = 0;
     for (size_t r = 0; r < n; r++) {
         hu[r] = acc;
@@ -1555,7 +1601,7 @@ int zdb_crc32_batch(const uint8_t *arena, size_t arena_len, const uint64_t *offs
     if (hipMemcpyAsync(h.arena, arena, arena_len, hipMemcpyHostToDevice, h.st) != hipSuccess ||
         hipMemcpyAsync(h.plan, h.hplan, n * 12 + (n + 1) * 8, hipMemcpyHostToDevice, h.st) != hipSuccess)
         return ZDB_CRC32_ELAUNCH;
-    rc = enqueue_batch(*c, h.arena, d_off, d_len, d_out, n, h.st, d_us);
+    rc = enqueue_batch(dev, *c, kv, h.arena, d_off, d_len, d_out, n, h.st, d_us);
     if (rc)
         return rc;
     if (hipMemcpyAsync(hout, d_out, n * 4, hipMemcpyDeviceToHost, h.st) != hipSuccess)
@@ -1596,22 +1642,22 @@ void zdb_crc32_host_free(void *p) {
 
 void zdb_crc32_set_timing(int enable) {
     std::lock_guard<std::mutex> g(g_mu);
-    g_timing = enable != 0;
+    g_timing.store(enable != 0);
 }
 
 static int drain_timing(float *each, size_t max_each, size_t *n_each) {
     size_t k = 0;
-    for (auto &p : g_pending) {
-        if (hipEventSynchronize(p.second) != hipSuccess)
+    for (const TimedLaunch &p : g_pending) {
+        if (hipEventSynchronize(p.e1) != hipSuccess)
             return ZDB_CRC32_ELAUNCH;
         float ms = 0;
-        hipEventElapsedTime(&ms, p.first, p.second);
+        hipEventElapsedTime(&ms, p.e0, p.e1);
         g_time_ms += ms;
         g_launches += 1;
         if (each && k < max_each)
             each[k++] = ms;
-        g_event_pool.push_back(p.first);
-        g_event_pool.push_back(p.second);
+        g_event_pool[p.dev].push_back(p.e0);
+        g_event_pool[p.dev].push_back(p.e1);
     }
     g_pending.clear();
     if (n_each)
@@ -1619,6 +1665,7 @@ static int drain_timing(float *each, size_t max_each, size_t *n_each) {
     return ZDB_CRC32_OK;
 }
 
+#ifdef ZDBCRC_DIAG
 // debug: per-launch kernel times (ms) recorded since the last drain
 long zdbcrc_debug_kernel_times(float *each, size_t max_each) {
     std::lock_guard<std::mutex> g(g_mu);
@@ -1629,6 +1676,8 @@ long zdbcrc_debug_kernel_times(float *each, size_t max_each) {
     g_launches = 0;
     return (long)k;
 }
+
+#endif // ZDBCRC_DIAG
 
 int zdb_crc32_kernel_stats(double *total_ms, uint64_t *launches) {
     std::lock_guard<std::mutex> g(g_mu);

@@ -26,7 +26,8 @@
  * visible GPU) -- datafiles are independent (records never span files,
  * api.c:300-303), so the scan shards with no device-to-device exchange.  The
  * exit status is the total mismatch count over all files (the reference's
- * per-file status, summed); a fatal error in one file (zdb_diep: short header
+ * per-file status, summed), saturated at 255 so that a multiple of 256 never
+ * reads as 0; a fatal error in one file (zdb_diep: short header
  * or payload, exit 1) ends the run after the reports of the files before it.
  *
  * Observable behaviour mirrored from the reference, per file:
@@ -633,5 +634,10 @@ int main(int argc, char *argv[]) {
     if (jobs > 1)
         for (int j = 0; j < jobs; j++)
             pthread_join(th[j], NULL);
+    /* one file: the reference's status (error count; the OS keeps its low 8
+     * bits, integrity-check.c:162-165).  Several files: saturate at 255 so a
+     * total that is a multiple of 256 cannot read as a clean store. */
+    if (s.nfiles > 1)
+        return total > 255 ? 255 : (int)total;
     return (int)(total > 0x7FFFFFFF ? 0x7FFFFFFF : total);
 }

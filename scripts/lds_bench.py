@@ -7,6 +7,9 @@ from pathlib import Path
 import numpy as np
 ROOT = Path(__file__).resolve().parents[1]
 sys.path[:0] = [str(ROOT / "0-db_amd")]
+# the diagnostic build: A/B variants and zdbcrc_debug_* hooks (not in libzdbcrc.so)
+import os as _os
+_os.environ.setdefault("ZDBCRC_LIB", str(ROOT / "0-db_amd" / "lib" / "libzdbcrc_diag.so"))
 import torch, zdbcrc
 f = zdbcrc._lib.zdbcrc_debug_lds_bench
 f.restype = C.c_float

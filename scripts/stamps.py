@@ -6,6 +6,9 @@ from pathlib import Path
 import numpy as np
 ROOT = Path(__file__).resolve().parents[1]
 sys.path[:0] = [str(ROOT / "0-db_amd")]
+# the diagnostic build: A/B variants and zdbcrc_debug_* hooks (not in libzdbcrc.so)
+import os as _os
+_os.environ.setdefault("ZDBCRC_LIB", str(ROOT / "0-db_amd" / "lib" / "libzdbcrc_diag.so"))
 import torch, zdbcrc
 sv = zdbcrc._lib.zdbcrc_debug_set_variant; sv.restype = C.c_char_p; sv.argtypes = [C.c_int]
 rd = zdbcrc._lib.zdbcrc_debug_read_stamps; rd.restype = C.c_int; rd.argtypes = [C.c_void_p, C.c_size_t]

@@ -355,6 +355,8 @@ def _check_real(img: np.ndarray, off: int, crc32) -> int:
     dlen = int(img[off + 1:off + 5].view("<u4")[0])
     integ = int(img[off + 9:off + 13].view("<u4")[0])
     p = off + 18 + idlen
+    if dlen == 0:  # read(fd, buf, 0) == 0 succeeds past EOF too: crc(empty) = 0
+        return int(integ == 0)
     if p + dlen > len(img):
         return -1
     return int(crc32(img[p:p + dlen]) == integ)
@@ -378,3 +380,21 @@ def test_batched_check_device(dev, oracle_c, name):
     np.testing.assert_array_equal(res.cpu().numpy(), want)
     if name.startswith("corrupt") or name == "multi_errors":
         assert (want[:len(recs)] == 0).any()
+
+
+@pytest.mark.parametrize("integrity,want", [(0, 1), (7, 0)])
+def test_batched_check_empty_payload_key_past_end(dev, oracle_c, integrity, want):
+    """An entry with datalength 0 whose key runs past the end of the image:
+    data_check_real's payload read of 0 bytes succeeds, so the result is
+    crc(empty) == integrity (data.c:546-570), not a short read."""
+    img = np.fromfile(GOLDEN / "datafiles" / "mixed.d0", dtype=np.uint8)
+    tail = np.frombuffer(dev.encode_entry(b"", 0, 28, integrity), np.uint8).copy()
+    tail[0] = 200  # idlength: the key would end 200 bytes past the image
+    full = np.concatenate([img, tail])
+    offs = [len(img)]
+    assert _check_real(full, len(img), oracle_c.crc32) == want
+    d_img = torch.from_numpy(full).cuda()
+    res = torch.full((1,), 7, dtype=torch.int32, device="cuda")
+    dev.datafile_check_device(d_img, torch.tensor(offs, dtype=torch.int64, device="cuda"), res)
+    torch.cuda.synchronize()
+    assert int(res.cpu()[0]) == want

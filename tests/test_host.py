@@ -34,6 +34,39 @@ def test_every_declared_symbol_is_exported():
         assert hasattr(zdbcrc._lib, name), name
 
 
+def test_library_exports_exactly_the_abi():
+    """libzdbcrc.so exports the include/*.h functions and nothing else: the
+    A/B kernel variants, probe kernels and zdbcrc_debug_* hooks live in
+    libzdbcrc_diag.so only (its version script), and no ZDBCRC_VARIANT knob
+    can reach the product."""
+    lib = ROOT / "0-db_amd" / "lib" / "libzdbcrc.so"
+    out = subprocess.run(["nm", "-D", "--defined-only", str(lib)], capture_output=True, text=True,
+                         check=True).stdout
+    exported = {ln.split()[-1] for ln in out.splitlines() if ln.strip()}
+    assert exported == _declared_functions()
+    blob = lib.read_bytes()
+    assert b"ZDBCRC_VARIANT" not in blob and b"zdbcrc_debug" not in blob
+    diag = ROOT / "0-db_amd" / "lib" / "libzdbcrc_diag.so"
+    dout = subprocess.run(["nm", "-D", "--defined-only", str(diag)], capture_output=True, text=True,
+                          check=True).stdout
+    assert "zdbcrc_debug_set_variant" in dout
+
+
+def test_host_batch_rejects_overflowing_descriptor_before_hip():
+    """zdb_crc32_batch: offset + length must not wrap around u64 (offset near
+    UINT64_MAX is EINVAL), and the check runs before HIP is initialised."""
+    code = ("import sys, numpy as np; sys.path.insert(0, %r); import zdbcrc; "
+            "a = np.zeros(64, np.uint8); o = np.array([2**64 - 2], np.uint64); "
+            "l = np.array([4], np.uint32); out = np.zeros(1, np.uint32); "
+            "rc = zdbcrc._batch_host(a.ctypes.data, a.size, o.ctypes.data, l.ctypes.data, out.ctypes.data, 1); "
+            "o3 = np.array([61], np.uint64); "
+            "rc3 = zdbcrc._batch_host(a.ctypes.data, a.size, o3.ctypes.data, l.ctypes.data, out.ctypes.data, 1); "
+            "print(rc, rc3, zdbcrc.gpu_initialized())"
+            % str(ROOT / "0-db_amd"))
+    out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, check=True)
+    assert out.stdout.split() == ["-2", "-2", "False"]
+
+
 def test_scalar_path_never_touches_hip():
     # key hashing / CHECK must not initialise the GPU (fork safety, SURVEY §0.9)
     code = ("import sys; sys.path.insert(0, %r); import zdbcrc; "

@@ -2,7 +2,7 @@
 store-wide scan): every file's report is byte-identical to the reference
 tool's run on that file (tests/golden/datafiles/*), reports come out in
 argument order whatever the number of worker threads, the exit status is the
-summed mismatch count, and a fatal file (short header / payload: zdb_diep in
+summed mismatch count (saturated at 255), and a fatal file (short header / payload: zdb_diep in
 the reference) ends the run after the reports of the files before it.
 Scalar engine here; the GPU engine runs the same checks in tests/test_gpu.py."""
 from __future__ import annotations
@@ -50,7 +50,8 @@ def check_multi(names, tmp: Path, engine: str, cases, extra=()):
     eerr = "".join(expected(n)[1] for n in names)
     assert out == eout
     assert err == eerr
-    assert code == sum(exits[n] for n in names) % 256
+    total = sum(exits[n] for n in names)
+    assert code == (total % 256 if len(names) == 1 else min(total, 255))
 
 
 @pytest.mark.parametrize("jobs", [1, 3, 16])
@@ -60,6 +61,16 @@ def test_multi_file_scan_cpu(tmp_path, datafile_cases, jobs):
 
 def test_multi_file_default_jobs_same_file_many_times(tmp_path, datafile_cases):
     check_multi(["multi_errors"] * 12, tmp_path, "cpu", datafile_cases)
+
+
+def test_multi_file_exit_status_saturates(tmp_path, datafile_cases):
+    """256 mismatches over 86 files: the status saturates at 255 instead of
+    wrapping to 0 (a corrupt store must never exit clean)."""
+    names = ["multi_errors"] * 85 + ["corrupt_crc"]
+    exits = {c["name"]: c["exit"] for c in datafile_cases}
+    assert sum(exits[n] for n in names) == 256
+    _, _, code = run_multi(names, tmp_path, "cpu", ["--jobs=8"])
+    assert code == 255
 
 
 @pytest.mark.parametrize("fatal", ["truncated_payload", "truncated_header"])
