@@ -84,6 +84,38 @@ def test_engine_value():
     assert zdbcrc.engine_value() == "sse42"
 
 
+@pytest.mark.parametrize("engine,flags", [("armv8", ["-msse4.2", "-DZDBCRC_ARMV8_EMULATE"]),
+                                          ("software", ["-mno-sse4.2"]),
+                                          ("sse42", ["-msse4.2"])])
+def test_every_engine_of_the_drop_in(tmp_path, kats, vectors, engine, flags):
+    """The three compile-time engines of crc32.c:94-155 (sse42, armv8,
+    software) built from crc32_cpu.c: engine name and values.  There is no
+    AArch64 compiler in this image, so the armv8 loop is built with its ACLE
+    intrinsics spelled by their SSE4.2 twins (ZDBCRC_ARMV8_EMULATE)."""
+    import ctypes as C
+    src = ROOT / "0-db_amd" / "csrc"
+    so = tmp_path / f"libcpu_{engine}.so"
+    subprocess.run(["gcc", "-O2", "-fPIC", "-shared", "-std=gnu11", "-I", str(ROOT / "include"), "-I", str(src),
+                    *flags, "-o", str(so), str(src / "crc32_cpu.c"), str(src / "crc32c_gf2.c"), "-lpthread"],
+                   check=True)
+    lib = C.CDLL(str(so))
+    lib.zdb_crc32_engine_value.restype = C.c_char_p
+    lib.zdb_crc32.restype = C.c_uint32
+    lib.zdb_crc32.argtypes = [C.c_void_p, C.c_ssize_t]
+    assert lib.zdb_crc32_engine_value().decode() == engine
+    for e in kats:
+        d = np.frombuffer(kat_bytes(e), np.uint8)
+        assert lib.zdb_crc32(d.ctypes.data if d.size else None, d.size) == int(e["crc"], 16), e["name"]
+    lens, seeds, crcs = vectors
+    for n, sd, c in list(zip(lens, seeds, crcs))[::7]:
+        if n > 70_000:
+            continue
+        buf = np.zeros(int(n) + 16, dtype=np.uint8)
+        for mis in (0, 3, 9):
+            buf[mis:mis + n] = oracle.splitmix_bytes(int(n), int(sd))
+            assert lib.zdb_crc32(buf[mis:].ctypes.data, int(n)) == int(c)
+
+
 def test_scalar_known_answers(kats):
     for e in kats:
         data = kat_bytes(e)
