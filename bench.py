@@ -9,8 +9,11 @@ checksums its own batch (different seed): weak scaling, no collective on the
 data path (torch.distributed is used only for the barrier and the max/sum of
 the timing).
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--workload zipf|fixed4k]
-  (N > 1: launched by torch.distributed.run, one rank per GPU)
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--workload zipf|fixed4k|c2u]
+  N > 1: either launched by torch.distributed.run (WORLD_SIZE must equal N),
+  or started plainly, in which case bench.py starts the N rank processes
+  itself (one per GPU) before touching any GPU.  Every rank checks its own
+  shard against the reference's digest of it (tests/golden/digests.json).
 
 Prints ONE JSON line on rank 0.
 """
@@ -196,14 +199,7 @@ def c4_leg(rank: int, world: int, steps: int, warmup: int, settle_s: float, barr
     n = len(lay["lens"])
     img, d_poff, d_len, expected, crcs = c4_build_device(lay, C4_SEED + rank)
     out = torch.empty(n, dtype=torch.int32, device="cuda")
-    parity = "unchecked"
-    gold = ROOT / "tests" / "golden" / "digests.json"
-    if rank == 0 and gold.exists():
-        ref = json.loads(gold.read_text()).get("C4")
-        got = digest(crcs)
-        if ref:
-            ok = all(got[k] == ref[k] for k in ("count", "xor", "crc_of_crcs"))
-            parity = "bit-exact vs reference digest C4" if ok else f"MISMATCH {got} vs {ref}"
+    parity = parity_of(digest(crcs), shard_digest_ref("C4", rank, 4.0), f"C4 shard {rank}")
     mism = torch.zeros(1024, dtype=torch.int32, device="cuda")
     cnt = torch.zeros(1, dtype=torch.int32, device="cuda")
 
@@ -239,7 +235,7 @@ def c4_leg(rank: int, world: int, steps: int, warmup: int, settle_s: float, barr
            "gibs": round(all_payload * steps / elapsed / GIB, 2),
            "ms_per_step": round(elapsed / steps * 1e3, 4), "kernel_ms": round(kern_s * 1e3, 4),
            "roofline_frac": round(alg / kern_s / 1e9 / HBM_PEAK_GBS, 4),
-           "mismatches": mismatches, "parity": parity}
+           "mismatches": mismatches, "parity_by_rank": gather_ranks(parity, world)}
     del img, out, expected
     torch.cuda.empty_cache()
     return res
@@ -438,6 +434,108 @@ def pmc_traffic(workload: str):
         return None
 
 
+def shard_digest_ref(kind: str, rank: int, gib: float) -> dict | None:
+    """The reference's digest of this rank's shard (tests/golden/digests.json,
+    computed by oracle/_ref in the build container: make_golden.py)."""
+    gold = ROOT / "tests" / "golden" / "digests.json"
+    if not gold.exists():
+        return None
+    d = json.loads(gold.read_text())
+    key = {("C3", 4.0): "C3_ranks", ("C3", 1 / 64): "C3_16MiB_ranks", ("C4", 4.0): "C4_ranks"}.get((kind, gib))
+    ranks = d.get(key, []) if key else []
+    if rank < len(ranks):
+        return ranks[rank]
+    if rank == 0 and kind in d and gib == 4.0:  # round-1 layout: rank 0 only
+        return d[kind]
+    return None
+
+
+def parity_of(got: dict, ref: dict | None, what: str) -> str:
+    if ref is None:
+        return "unchecked (no reference digest for this shard)"
+    ok = all(got[k] == ref[k] for k in ("count", "xor", "crc_of_crcs"))
+    return f"bit-exact vs reference digest {what}" if ok else f"MISMATCH {got} vs {ref}"
+
+
+def summarize_parity(parities: list) -> str:
+    if len(parities) == 1:
+        return parities[0]
+    bad = [i for i, p in enumerate(parities) if not p.startswith("bit-exact")]
+    if not bad:
+        return f"bit-exact vs reference digests on all {len(parities)} shards"
+    return f"NOT bit-exact (or unchecked) on ranks {bad}: see parity_by_rank"
+
+
+def gather_ranks(obj, world: int) -> list:
+    """every rank's small result object on every rank (parity strings)"""
+    if world == 1:
+        return [obj]
+    import torch.distributed as dist
+    out = [None] * world
+    dist.all_gather_object(out, obj)
+    return out
+
+
+def launch_ranks(args) -> int:
+    """`python bench.py --gpus N` outside torch.distributed.run: start N rank
+    processes (one per GPU) before this process touches any GPU, with the
+    environment torchrun would give them, and return the worst exit code.
+    Only rank 0 prints the JSON line."""
+    import socket
+    import subprocess
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    procs = []
+    for r in range(args.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus),
+                   LOCAL_WORLD_SIZE=str(args.gpus), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, str(Path(__file__).resolve())] + sys.argv[1:], env=env))
+    rc = 0
+    for p in procs:
+        rc = max(rc, p.wait())
+    return rc
+
+
+def cpu_rank(args, rank: int, world: int) -> None:
+    """--device cpu: the multi-rank plumbing on the CPU (gloo), for the
+    world-size-2 test -- each rank checksums its own C3 shard with the scalar
+    drop-in engine and checks it against the reference digest of that shard;
+    the timing and aggregation are the GPU path's (combine_ranks)."""
+    import torch.distributed as dist
+    import zdbcrc
+    if world > 1:
+        dist.init_process_group("gloo")
+    target = int(args.gib * (1 << 30))
+    offs, lens, seed, desc = make_dataset(args.workload, target, rank)
+    arena = zdbcrc.synth_fill(int(offs[-1] + lens[-1]), seed)
+    crcs = np.array([zdbcrc.crc32(arena[o:o + l]) for o, l in zip(offs, lens)], dtype=np.uint32)
+    parity = parity_of(digest(crcs), shard_digest_ref("C3", rank, args.gib), f"C3 shard {rank}")
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        for o, l in zip(offs, lens):
+            zdbcrc.crc32(arena[o:o + l])
+    t1 = time.perf_counter()
+    if world > 1:
+        dist.barrier()
+    payload = int(lens.sum())
+    elapsed, all_payload = combine_ranks(t1 - t0, payload, world)
+    parities = gather_ranks(parity, world)
+    if rank == 0:
+        print(json.dumps({
+            "metric": METRIC, "value": round(all_payload * args.steps / elapsed / GIB, 4), "unit": "GiB/s",
+            "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "u8", "data": "synthetic", "device": "cpu (plumbing test: scalar engine)",
+            "config": {"workload": desc, "records_per_gpu": len(lens), "payload_bytes_per_gpu": payload,
+                       "parallelism": f"{world} independent shards, no data-path collective"},
+            "parity": summarize_parity(parities), "parity_by_rank": parities}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -451,11 +549,22 @@ def main():
     ap.add_argument("--no-c4", action="store_true", help="skip the C4 integrity-scan leg")
     ap.add_argument("--settle-s", type=float, default=1.0,
                     help="untimed steps after the warmup until this many seconds have passed")
+    ap.add_argument("--device", default="gpu", choices=["gpu", "cpu"],
+                    help="cpu: multi-rank plumbing test on gloo with the scalar engine (tests only)")
     args = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ:
+        if args.gpus > 1:
+            sys.exit(launch_ranks(args))
+    elif int(os.environ["WORLD_SIZE"]) != args.gpus:
+        sys.exit(f"bench.py: WORLD_SIZE={os.environ['WORLD_SIZE']} but --gpus {args.gpus}: refusing to measure "
+                 "a different number of GPUs than asked for")
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.device == "cpu":
+        cpu_rank(args, rank, world)
+        return
 
     import torch
     import torch.distributed as dist
@@ -485,20 +594,17 @@ def main():
     def step():
         zdbcrc.batch_device(arena, d_offs, d_lens, out)
 
-    # parity at full size: rank 0's batch is the golden dataset
+    # parity at full size: every rank's shard against the reference's digest of it
     step()
     torch.cuda.synchronize()
-    parity = "unchecked"
-    gold = ROOT / "tests" / "golden" / "digests.json"
-    if rank == 0 and gold.exists():
-        key = {"zipf": "C3", "fixed4k": "C2"}.get(args.workload)
-        ref = json.loads(gold.read_text()).get(key) if key else None
-        got = digest(out.cpu().numpy().view(np.uint32))
-        if ref and abs(args.gib - 4.0) < 1e-9:
-            ok = all(got[k] == ref[k] for k in ("count", "xor", "crc_of_crcs"))
-            parity = f"bit-exact vs reference digest {key}" if ok else f"MISMATCH {got} vs {ref}"
-            log(f"parity: {parity}")
-
+    got = digest(out.cpu().numpy().view(np.uint32))
+    if args.workload == "zipf":
+        parity = parity_of(got, shard_digest_ref("C3", rank, args.gib), f"C3 shard {rank}")
+    elif args.workload == "fixed4k" and rank == 0 and args.gib == 4.0:
+        parity = parity_of(got, json.loads((ROOT / "tests/golden/digests.json").read_text()).get("C2"), "C2")
+    else:
+        parity = "unchecked (no reference digest for this shard)"
+    log(f"rank {rank} parity: {parity}")
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
@@ -581,6 +687,7 @@ def main():
         log("timing the CPU baseline")
         cpu = cpu_baseline(offs, lens, seed, args.cpu_seconds)
 
+    parities = gather_ranks(parity, world)
     if rank == 0:
         line = {
             "metric": METRIC, "value": round(value, 2), "unit": "GiB/s", "n_gpus": world,
@@ -590,7 +697,7 @@ def main():
             "data": "synthetic (splitmix64 bytes; SURVEY §8(d) Zipf sizes), resident in HBM",
             "config": {"workload": desc, "records_per_gpu": n, "payload_bytes_per_gpu": payload,
                        "parallelism": f"{world} independent shards, no data-path collective"},
-            "parity": parity, "roofline": roofline, "cpu_baseline": cpu, "extra": extra,
+            "parity": summarize_parity(parities), "parity_by_rank": parities, "roofline": roofline, "cpu_baseline": cpu, "extra": extra,
         }
         print(json.dumps(line), flush=True)
     if world > 1:

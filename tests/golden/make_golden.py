@@ -210,10 +210,51 @@ def digest_c4(ref: oracle.Reference) -> dict:
             "image_bytes": lay["total"], "payload_bytes": int(lay["lens"].sum()), **digest(ref, c4)}
 
 
+def c3_shard_digest(ref: oracle.Reference, rank: int, target: int) -> dict:
+    """bench.make_dataset("zipf", target, rank): rank r's C3 shard"""
+    import zdbcrc
+    sys.path.insert(0, str(ROOT))
+    import bench
+    offs, lens, seed, _ = bench.make_dataset("zipf", target, rank)
+    total = int(offs[-1] + lens[-1])
+    arena = zdbcrc.synth_fill(total, seed)
+    crcs = ref.batch(arena, offs.astype(np.uint64), lens.astype(np.uint32), threads=8)
+    return {"rank": rank, "seed": seed, "target": target, "total_bytes": total, **digest(ref, crcs)}
+
+
+def c4_shard_digest(ref: oracle.Reference, rank: int) -> dict:
+    import zdbcrc
+    sys.path.insert(0, str(ROOT))
+    import bench
+    lay = bench.c4_layout(rank)
+    arena = zdbcrc.synth_fill(lay["total"], bench.C4_SEED + rank)
+    c4 = ref.batch(arena, lay["payload_off"].astype(np.uint64), lay["lens"].astype(np.uint32), threads=8)
+    return {"rank": rank, "seed": bench.C4_SEED + rank, "files": len(lay["file_off"]), "image_bytes": lay["total"],
+            "payload_bytes": int(lay["lens"].sum()), **digest(ref, c4)}
+
+
+def rank_digests(ref: oracle.Reference, ranks: int = 8) -> dict:
+    """every rank's shard of a multi-GPU bench run (bench.py --gpus N, N <= 8):
+    the full-size C3 (4 GiB) and C4 (64 datafiles) shards, and the 16 MiB C3
+    shards the CPU-mode plumbing test (tests/test_dist.py) runs"""
+    out = {"C3_ranks": [], "C4_ranks": [], "C3_16MiB_ranks": []}
+    for r in range(ranks):
+        out["C3_16MiB_ranks"].append(c3_shard_digest(ref, r, 16 << 20))
+        out["C3_ranks"].append(c3_shard_digest(ref, r, 4 << 30))
+        out["C4_ranks"].append(c4_shard_digest(ref, r))
+        print(f"  rank {r}: C3 {out['C3_ranks'][-1]['xor']} C4 {out['C4_ranks'][-1]['xor']}", flush=True)
+    return out
+
+
 def main():
     ref = oracle.Reference()
     assert ref.engine() == "sse42", ref.engine()
     OUT.mkdir(parents=True, exist_ok=True)
+    if "--only-rank-digests" in sys.argv:  # add / refresh the per-rank shard digests
+        d = json.loads((OUT / "digests.json").read_text())
+        d.update(rank_digests(ref))
+        (OUT / "digests.json").write_text(json.dumps(d, indent=1) + "\n")
+        return
     if "--only-c4" in sys.argv:  # add / refresh the C4 digest only
         d = json.loads((OUT / "digests.json").read_text())
         d["C4"] = digest_c4(ref)

@@ -5,8 +5,10 @@ checksums need no exchange (the scalar drop-in engine stands in for the GPU
 here; the GPU path is covered by tests/test_gpu.py)."""
 from __future__ import annotations
 
+import json
 import os
 import socket
+import subprocess
 import sys
 
 import numpy as np
@@ -55,3 +57,28 @@ def test_two_rank_shards_and_aggregation():
     assert tot0 == tot1 == float(b0 + b1)          # whole-job bytes
     import bench
     assert s0 == bench.C3_SEED                     # rank 0 == golden C3 recipe
+
+
+def test_bench_spawns_its_own_ranks():
+    """`python bench.py --gpus 2` started plainly (no torchrun) launches two
+    rank processes itself; both check their own shard against the
+    reference's digest of it, and rank 0 reports the whole job (n_gpus 2)."""
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT")}
+    p = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--gpus", "2", "--device", "cpu",
+                        "--gib", str(1 / 64), "--steps", "1", "--warmup", "0"],
+                       capture_output=True, text=True, timeout=300, env=env)
+    assert p.returncode == 0, p.stderr[-2000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1  # only rank 0 prints
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2
+    assert d["parity_by_rank"] == ["bit-exact vs reference digest C3 shard 0",
+                                   "bit-exact vs reference digest C3 shard 1"]
+    assert d["parity"] == "bit-exact vs reference digests on all 2 shards"
+
+
+def test_bench_refuses_world_size_mismatch():
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    p = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--gpus", "2", "--device", "cpu"],
+                       capture_output=True, text=True, timeout=120, env=env)
+    assert p.returncode != 0 and "WORLD_SIZE=1" in p.stderr
