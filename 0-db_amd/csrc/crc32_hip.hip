@@ -1349,6 +1349,7 @@ const char *zdb_crc32_strerror(int code) {
     case ZDB_CRC32_EINVAL: return "invalid argument";
     case ZDB_CRC32_ENOMEM: return "device allocation failed";
     case ZDB_CRC32_ELAUNCH: return "HIP launch/runtime error";
+    case ZDB_CRC32_ENOSPC: return "output buffers too small";
     default: return "unknown error";
     }
 }
@@ -1365,6 +1366,10 @@ const char *zdb_crc32_batch_engine(void) {
 }
 
 int zdb_crc32_gpu_initialized(void) { return g_hip_touched ? 1 : 0; }
+
+// library-internal (not in the version script): other HIP objects of
+// libzdbcrc.so record that they initialised HIP
+void zdbcrc_internal_mark_hip(void) { g_hip_touched = true; }
 
 #ifdef ZDBCRC_DIAG
 // measurement hook (not part of the public ABI): time a read-only stream of

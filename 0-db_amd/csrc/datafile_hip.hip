@@ -1,0 +1,448 @@
+// datafile_hip.hip -- f3: record-boundary discovery for 0-db datafile images
+// resident in HBM, and the device-resident integrity scan built on it
+// (tools/integrity-check over a whole store, integrity-check.c:59-105).
+//
+// The reference finds records with a serial chain: each entry header gives
+// the next offset, pos' = pos + 18 + idlength + datalength
+// (integrity-check.c:59-69, data.c:306-311; host form: datafile.c).  A GPU
+// cannot follow one chain fast (one dependent HBM round trip per record), so
+// every file is cut into chunks of C bytes (default 4 MiB) and the chain is
+// discovered speculatively and stitched exactly:
+//
+//   A1 search  (one wave per chunk): the first position p >= chunk start
+//              that looks like an entry header -- datalength <= 8 MiB (the
+//              writer's cap, data.h:6), flags <= 3 (data.h:47-51) -- and whose
+//              successor q = p + 18 + idlength + datalength names p as its
+//              `previous` entry (data_insert, data.c:601), or ends the file.
+//              64 lanes x 16 positions per 1 KiB step; a random position
+//              passes the cheap filter with p ~ 2^-15 and the back-pointer
+//              check with p ~ 2^-32.
+//   A2 walk    (one thread per chunk, 64 chains in flight per wave): follow
+//              the chain from that candidate to the first header at or past
+//              the chunk end (its "exit"), counting records, stopping on the
+//              serial walk's terminal conditions (clean EOF, short header,
+//              short payload).
+//   B  stitch  (one thread per file): chunk 0 starts at offset 28, exactly
+//              where the reference starts.  Chunk c is accepted when its
+//              speculative start equals the true exit of chunk c-1; a chunk
+//              that no record starts in is skipped; otherwise (a false
+//              candidate, or a true header the filter rejected: a file not
+//              written by zdbd, a rewritten `previous` chain) the chunk is
+//              re-walked serially from the true exit.  So the result is the
+//              serial walk's, whatever the filter decides -- the filter only
+//              decides how much is parallel.
+//   B2 prefix  record counts of the files -> global record index base.
+//   C  emit    (one thread per chunk): re-follow the accepted chain and write
+//              the descriptors in file order.
+//
+// The integrity scan then verifies the emitted descriptors with the batched
+// checksum kernel (zdb_crc32_verify_device).  Bytes per record: ~3 header
+// reads of a few bytes (A2, C) + the search windows (on average the
+// remainder of the record straddling each chunk start).
+
+#include <cstdint>
+#include <cstring>
+#include <map>
+#include <mutex>
+
+#include <hip/hip_runtime.h>
+
+#include "zdb_crc32.h"
+#include "zdb_datafile.h"
+
+extern "C" void zdbcrc_internal_mark_hip(void); // crc32_hip.hip (not exported)
+
+namespace {
+
+constexpr uint64_t NONE = ~0ull;
+constexpr int32_t ST_CONTINUE = -1;
+constexpr uint32_t FILTER_MAX_PAYLOAD = 8u << 20; // ZDB_DATA_MAX_PAYLOAD, data.h:6 (filter only)
+constexpr uint32_t FILTER_MAX_FLAGS = 3;          // DELETED | TRUNCATED, data.h:47-51 (filter only)
+constexpr uint32_t DEFAULT_LG_CHUNK = 22;         // 4 MiB
+constexpr uint32_t WALK_T = 256;
+
+// little-endian u32 at any byte address: two aligned dword loads + one
+// v_alignbyte (reads up to 7 bytes past p; images are readable 16 bytes past
+// their end, as for the checksum kernel)
+__device__ __forceinline__ uint32_t ld_le32(const uint8_t *p) {
+    const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+    const uint32_t *q = reinterpret_cast<const uint32_t *>(a & ~uintptr_t(3));
+    return __builtin_amdgcn_alignbyte(q[1], q[0], (uint32_t)(a & 3));
+}
+
+// one record of the serial walk at pos (datafile.c zdb_datafile_walk):
+// SHORT_HEADER -> not a record; SHORT_PAYLOAD -> a record that ends the walk
+__device__ __forceinline__ int32_t hop(const uint8_t *f, uint64_t len, uint64_t pos, uint64_t &next,
+                                       uint32_t &L) {
+    const uint64_t hlen = ZDB_ENTRY_HEADER_SIZE + (uint64_t)f[pos];
+    if (pos + hlen > len)
+        return ZDB_WALK_SHORT_HEADER;
+    L = ld_le32(f + pos + 1);
+    next = pos + hlen;
+    if (L) {
+        if (next + L > len)
+            return ZDB_WALK_SHORT_PAYLOAD;
+        next += L;
+    }
+    return ST_CONTINUE;
+}
+
+// follow the chain from pos while pos < cend; EMIT writes the records
+template <bool EMIT>
+__device__ __forceinline__ void walk_chain(const uint8_t *f, uint64_t len, uint64_t foff, uint64_t pos, uint64_t cend,
+                                           uint32_t &count, uint64_t &exit, int32_t &st, uint64_t idx,
+                                           uint64_t capacity, uint64_t *__restrict__ entry_off,
+                                           uint64_t *__restrict__ poff, uint32_t *__restrict__ plen,
+                                           uint32_t *__restrict__ expect) {
+    count = 0;
+    st = ST_CONTINUE;
+    while (pos < cend) {
+        if (pos >= len) { // clean end of file (pos == len)
+            st = ZDB_WALK_OK;
+            break;
+        }
+        uint64_t next = 0;
+        uint32_t L = 0;
+        const int32_t s = hop(f, len, pos, next, L);
+        if (s == ZDB_WALK_SHORT_HEADER) {
+            st = s;
+            break;
+        }
+        if (EMIT && idx < capacity) {
+            const bool full = s == ST_CONTINUE && L > 0; // payload present and non-empty
+            entry_off[idx] = foff + pos;
+            poff[idx] = foff + pos + ZDB_ENTRY_HEADER_SIZE + f[pos];
+            plen[idx] = full ? L : 0u;
+            expect[idx] = full ? ld_le32(f + pos + 9) : 0u; // empty payloads are skipped (integrity-check.c:81-82)
+        }
+        idx++;
+        count++;
+        if (s == ZDB_WALK_SHORT_PAYLOAD) {
+            st = s;
+            break;
+        }
+        pos = next;
+    }
+    if (st == ST_CONTINUE && pos >= len)
+        st = ZDB_WALK_OK;
+    exit = pos;
+}
+
+// is there an entry header at p whose chain is consistent one step ahead?
+__device__ __forceinline__ bool plausible_successor(const uint8_t *f, uint64_t len, uint64_t p, uint32_t idl,
+                                                    uint32_t L) {
+    const uint64_t q = p + ZDB_ENTRY_HEADER_SIZE + idl + L;
+    if (q == len)
+        return true;
+    if (q + ZDB_ENTRY_HEADER_SIZE > len)
+        return false;
+    return ld_le32(f + q + 5) == (uint32_t)p; // q's `previous` (data.h:59)
+}
+
+struct FileTab {
+    const uint8_t *image;
+    const uint64_t *file_off;
+    const uint64_t *file_len;
+    uint32_t nfiles;
+    uint32_t cpf; // chunks per file (grid)
+    uint32_t lg;  // log2 chunk bytes
+};
+
+// A1: speculative start of every chunk (one wave per chunk)
+__global__ __launch_bounds__(WALK_T) void walk_search_kernel(FileTab t, uint64_t *__restrict__ s_start,
+                                                             int32_t *__restrict__ s_status) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint64_t w = (uint64_t)blockIdx.x * (WALK_T / 64) + (threadIdx.x >> 6);
+    if (w >= (uint64_t)t.nfiles * t.cpf)
+        return;
+    const uint32_t fi = (uint32_t)(w / t.cpf), c = (uint32_t)(w % t.cpf);
+    const uint64_t len = t.file_len[fi];
+    const uint8_t *f = t.image + t.file_off[fi];
+    const uint64_t C = 1ull << t.lg, c0 = (uint64_t)c * C;
+    uint64_t start = NONE;
+    int32_t st = ST_CONTINUE;
+    if (c == 0) {
+        // data_descriptor_load / _validate (data.c:177-209): 28-byte header,
+        // magic "DAT0", version 3
+        const bool bad = len < ZDB_DATA_HEADER_SIZE || f[0] != 'D' || f[1] != 'A' || f[2] != 'T' ||
+                         f[3] != '0' || ld_le32(f + 4) != ZDB_DATAFILE_VERSION;
+        if (bad)
+            st = ZDB_WALK_BAD_DESCRIPTOR;
+        else
+            start = ZDB_DATA_HEADER_SIZE;
+    } else if (c0 < len && len >= ZDB_ENTRY_HEADER_SIZE) {
+        // positions p in [c0, c0 + C) with a whole 18-byte header in the file
+        const uint64_t lim = (c0 + C < len - (ZDB_ENTRY_HEADER_SIZE - 1)) ? c0 + C : len - (ZDB_ENTRY_HEADER_SIZE - 1);
+        for (uint64_t b = c0; b < lim && start == NONE; b += 1024) {
+            const uint64_t p0 = b + 16u * lane; // c0 is a multiple of C >= 1 KiB: 16-byte aligned
+            uint32_t m = 0;
+            uint32_t wv[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+            if (p0 < lim) {
+                const uint4 a0 = *reinterpret_cast<const uint4 *>(f + p0);
+                const uint4 a1 = *reinterpret_cast<const uint4 *>(f + p0 + 16);
+                wv[0] = a0.x; wv[1] = a0.y; wv[2] = a0.z; wv[3] = a0.w;
+                wv[4] = a1.x; wv[5] = a1.y; wv[6] = a1.z; wv[7] = a1.w;
+#pragma unroll
+                for (int k = 0; k < 16; k++) {
+                    const int d = (k + 1) >> 2, sh = (k + 1) & 3;
+                    const uint32_t L = __builtin_amdgcn_alignbyte(wv[d + 1], wv[d], (uint32_t)sh);
+                    const uint32_t flags = (wv[(k + 13) >> 2] >> (8 * ((k + 13) & 3))) & 0xFFu;
+                    m |= (uint32_t)(L <= FILTER_MAX_PAYLOAD && flags <= FILTER_MAX_FLAGS) << k;
+                }
+                const uint64_t room = lim - p0; // positions p0 + k < lim
+                if (room < 16)
+                    m &= (1u << room) - 1u;
+            }
+            uint64_t found = NONE;
+            while (m) {
+                const int k = __builtin_ctz(m);
+                m &= m - 1;
+                const int d = (k + 1) >> 2, sh = (k + 1) & 3;
+                const uint32_t L = __builtin_amdgcn_alignbyte(wv[d + 1], wv[d], (uint32_t)sh);
+                const uint32_t idl = (wv[k >> 2] >> (8 * (k & 3))) & 0xFFu;
+                if (plausible_successor(f, len, p0 + k, idl, L)) {
+                    found = p0 + k;
+                    break;
+                }
+            }
+            const uint64_t hit = __ballot(found != NONE);
+            if (hit) { // lanes hold increasing addresses: the lowest lane has the first candidate
+                const uint32_t l = (uint32_t)__builtin_ctzll(hit);
+                start = ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(found >> 32), l) << 32) |
+                        __builtin_amdgcn_readlane((uint32_t)found, l);
+            }
+        }
+    }
+    if (lane == 0) {
+        s_start[w] = start;
+        s_status[w] = st;
+    }
+}
+
+// A2: speculative chain of every chunk (one thread per chunk)
+__global__ __launch_bounds__(WALK_T) void walk_spec_kernel(FileTab t, const uint64_t *__restrict__ s_start,
+                                                           uint64_t *__restrict__ s_exit, uint32_t *__restrict__ s_count,
+                                                           int32_t *__restrict__ s_status) {
+    const uint64_t w = (uint64_t)blockIdx.x * WALK_T + threadIdx.x;
+    if (w >= (uint64_t)t.nfiles * t.cpf)
+        return;
+    const uint64_t start = s_start[w];
+    if (start == NONE)
+        return;
+    const uint32_t fi = (uint32_t)(w / t.cpf), c = (uint32_t)(w % t.cpf);
+    const uint64_t len = t.file_len[fi];
+    const uint64_t cend = ((uint64_t)c + 1) << t.lg;
+    uint32_t count;
+    uint64_t exit;
+    int32_t st;
+    walk_chain<false>(t.image + t.file_off[fi], len, 0, start, cend, count, exit, st, 0, 0, nullptr, nullptr,
+                      nullptr, nullptr);
+    s_exit[w] = exit;
+    s_count[w] = count;
+    s_status[w] = st;
+}
+
+// B: exact stitch (one thread per file); re-walks a chunk serially when its
+// speculative start is not the true exit of the chunk before it
+__global__ __launch_bounds__(WALK_T) void walk_stitch_kernel(FileTab t, const uint64_t *__restrict__ s_start,
+                                                             const uint64_t *__restrict__ s_exit,
+                                                             const uint32_t *__restrict__ s_count,
+                                                             const int32_t *__restrict__ s_status,
+                                                             uint64_t *__restrict__ true_start,
+                                                             uint64_t *__restrict__ chunk_base,
+                                                             uint64_t *__restrict__ file_records,
+                                                             int32_t *__restrict__ file_status,
+                                                             uint32_t *__restrict__ rewalks) {
+    const uint32_t fi = blockIdx.x * WALK_T + threadIdx.x;
+    if (fi >= t.nfiles)
+        return;
+    const uint64_t len = t.file_len[fi];
+    const uint8_t *f = t.image + t.file_off[fi];
+    const uint64_t w0 = (uint64_t)fi * t.cpf;
+    uint64_t total = 0;
+    int32_t st = ST_CONTINUE;
+    uint64_t pos = 0;
+    uint32_t redo = 0;
+    if (len > ((uint64_t)t.cpf << t.lg)) { // longer than the caller's max_file_len bound
+        st = ZDB_WALK_EXCEEDS_BOUND;
+    } else if (s_status[w0] == ZDB_WALK_BAD_DESCRIPTOR) {
+        st = ZDB_WALK_BAD_DESCRIPTOR;
+    } else {
+        pos = ZDB_DATA_HEADER_SIZE; // chunk 0 starts where the reference starts
+    }
+    for (uint32_t c = 0; c < t.cpf; c++) {
+        const uint64_t w = w0 + c;
+        const uint64_t cend = ((uint64_t)c + 1) << t.lg;
+        chunk_base[w] = total;
+        if (st != ST_CONTINUE || pos >= cend) { // walk over, or no record starts in this chunk
+            true_start[w] = NONE;
+            continue;
+        }
+        true_start[w] = pos;
+        uint32_t count;
+        uint64_t exit;
+        int32_t cs;
+        if (s_start[w] == pos) {
+            count = s_count[w];
+            exit = s_exit[w];
+            cs = s_status[w];
+        } else {
+            walk_chain<false>(f, len, 0, pos, cend, count, exit, cs, 0, 0, nullptr, nullptr, nullptr, nullptr);
+            redo++;
+        }
+        total += count;
+        pos = exit;
+        st = cs;
+    }
+    file_records[fi] = total;
+    file_status[fi] = st == ST_CONTINUE ? ZDB_WALK_OK : st;
+    rewalks[fi] = redo;
+}
+
+// B2: record counts -> global record base of every file, in place
+// (exclusive prefix; entry nfiles = total)
+__global__ void walk_prefix_kernel(uint32_t nfiles, uint64_t *__restrict__ file_records,
+                                   uint32_t *__restrict__ rewalks) {
+    if (threadIdx.x != 0 || blockIdx.x != 0)
+        return;
+    uint64_t acc = 0;
+    uint32_t redo = 0;
+    for (uint32_t i = 0; i < nfiles; i++) {
+        const uint64_t n = file_records[i];
+        file_records[i] = acc;
+        acc += n;
+        redo += rewalks[i];
+    }
+    file_records[nfiles] = acc;
+    rewalks[nfiles] = redo;
+}
+
+// C: descriptors in file order (one thread per chunk)
+__global__ __launch_bounds__(WALK_T) void walk_emit_kernel(FileTab t, const uint64_t *__restrict__ true_start,
+                                                           const uint64_t *__restrict__ chunk_base,
+                                                           const uint64_t *__restrict__ file_base, uint64_t capacity,
+                                                           uint64_t *__restrict__ entry_off, uint64_t *__restrict__ poff,
+                                                           uint32_t *__restrict__ plen,
+                                                           uint32_t *__restrict__ expect) {
+    const uint64_t w = (uint64_t)blockIdx.x * WALK_T + threadIdx.x;
+    if (w >= (uint64_t)t.nfiles * t.cpf)
+        return;
+    const uint64_t start = true_start[w];
+    if (start == NONE)
+        return;
+    const uint32_t fi = (uint32_t)(w / t.cpf), c = (uint32_t)(w % t.cpf);
+    const uint64_t cend = ((uint64_t)c + 1) << t.lg;
+    const uint64_t foff = t.file_off[fi];
+    uint32_t count;
+    uint64_t exit;
+    int32_t st;
+    walk_chain<true>(t.image + foff, t.file_len[fi], foff, start, cend, count, exit, st,
+                     file_base[fi] + chunk_base[w], capacity, entry_off, poff, plen, expect);
+}
+
+// per (device, stream) workspace of the walk
+struct WalkWs {
+    void *ptr = nullptr;
+    size_t bytes = 0;
+};
+std::mutex g_walk_mu[64];
+std::map<void *, WalkWs> g_walk_ws[64];
+
+} // namespace
+
+extern "C" {
+
+int zdb_datafile_walk_device(const uint8_t *d_image, const uint64_t *d_file_off, const uint64_t *d_file_len,
+                             uint32_t nfiles, uint64_t max_file_len, uint32_t chunk_bytes, uint64_t *d_entry_off,
+                             uint64_t *d_payload_off, uint32_t *d_payload_len, uint32_t *d_expected,
+                             uint64_t capacity, uint64_t *d_file_records, int32_t *d_file_status,
+                             uint32_t *d_rewalks, void *stream) {
+    if (nfiles == 0)
+        return ZDB_CRC32_OK;
+    if (!d_image || !d_file_off || !d_file_len || !d_file_records || !d_file_status || !d_rewalks)
+        return ZDB_CRC32_EINVAL;
+    if (capacity && (!d_entry_off || !d_payload_off || !d_payload_len || !d_expected))
+        return ZDB_CRC32_EINVAL;
+    uint32_t lg = DEFAULT_LG_CHUNK;
+    if (chunk_bytes) {
+        if (chunk_bytes < 1024 || (chunk_bytes & (chunk_bytes - 1)))
+            return ZDB_CRC32_EINVAL; // a power of two >= 1 KiB (the search step)
+        lg = (uint32_t)__builtin_ctz(chunk_bytes);
+    }
+    if (max_file_len > (1ull << 32)) // datafile offsets are u32 (data.h:59, index.h:54)
+        return ZDB_CRC32_EINVAL;
+    const uint64_t cpf64 = max_file_len ? (max_file_len + (1ull << lg) - 1) >> lg : 1;
+    const uint64_t nchunks = cpf64 * nfiles;
+    if (nchunks > (1ull << 31))
+        return ZDB_CRC32_EINVAL;
+    zdbcrc_internal_mark_hip();
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64)
+        return ZDB_CRC32_ENODEV;
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    std::lock_guard<std::mutex> g(g_walk_mu[dev]);
+    // workspace: per chunk s_start, s_exit, true_start, chunk_base (u64),
+    // s_count (u32), s_status (i32)
+    auto al = [](size_t x) { return (x + 255) & ~size_t(255); };
+    const size_t need = 4 * al(nchunks * 8) + 2 * al(nchunks * 4);
+    WalkWs &ws = g_walk_ws[dev][stream];
+    if (ws.bytes < need) {
+        if (ws.ptr) {
+            hipStreamSynchronize(st);
+            hipFree(ws.ptr);
+            ws.ptr = nullptr;
+            ws.bytes = 0;
+        }
+        if (hipMalloc(&ws.ptr, need) != hipSuccess)
+            return ZDB_CRC32_ENOMEM;
+        ws.bytes = need;
+    }
+    uint8_t *b = static_cast<uint8_t *>(ws.ptr);
+    uint64_t *s_start = reinterpret_cast<uint64_t *>(b);
+    uint64_t *s_exit = reinterpret_cast<uint64_t *>(b + al(nchunks * 8));
+    uint64_t *true_start = reinterpret_cast<uint64_t *>(b + 2 * al(nchunks * 8));
+    uint64_t *chunk_base = reinterpret_cast<uint64_t *>(b + 3 * al(nchunks * 8));
+    uint32_t *s_count = reinterpret_cast<uint32_t *>(b + 4 * al(nchunks * 8));
+    int32_t *s_status = reinterpret_cast<int32_t *>(b + 4 * al(nchunks * 8) + al(nchunks * 4));
+
+    const FileTab t{d_image, d_file_off, d_file_len, nfiles, (uint32_t)cpf64, lg};
+    const uint32_t waves_per_block = WALK_T / 64;
+    hipLaunchKernelGGL(walk_search_kernel, dim3((uint32_t)((nchunks + waves_per_block - 1) / waves_per_block)),
+                       dim3(WALK_T), 0, st, t, s_start, s_status);
+    const dim3 gch((uint32_t)((nchunks + WALK_T - 1) / WALK_T));
+    hipLaunchKernelGGL(walk_spec_kernel, gch, dim3(WALK_T), 0, st, t, s_start, s_exit, s_count, s_status);
+    hipLaunchKernelGGL(walk_stitch_kernel, dim3((nfiles + WALK_T - 1) / WALK_T), dim3(WALK_T), 0, st, t, s_start,
+                       s_exit, s_count, s_status, true_start, chunk_base, d_file_records, d_file_status, d_rewalks);
+    hipLaunchKernelGGL(walk_prefix_kernel, dim3(1), dim3(64), 0, st, nfiles, d_file_records, d_rewalks);
+    if (capacity)
+        hipLaunchKernelGGL(walk_emit_kernel, gch, dim3(WALK_T), 0, st, t, true_start, chunk_base, d_file_records,
+                           capacity, d_entry_off, d_payload_off, d_payload_len, d_expected);
+    return hipGetLastError() == hipSuccess ? ZDB_CRC32_OK : ZDB_CRC32_ELAUNCH;
+}
+
+int zdb_datafile_scan_device(const uint8_t *d_image, const uint64_t *d_file_off, const uint64_t *d_file_len,
+                             uint32_t nfiles, uint64_t max_file_len, uint32_t chunk_bytes,
+                             const zdb_scan_buffers_t *b, uint64_t *n_records, void *stream) {
+    if (!b || !n_records || !b->file_records || !b->mismatch_count || (b->max_mismatch && !b->mismatch))
+        return ZDB_CRC32_EINVAL;
+    *n_records = 0;
+    int rc = zdb_datafile_walk_device(d_image, d_file_off, d_file_len, nfiles, max_file_len, chunk_bytes,
+                                      b->entry_off, b->payload_off, b->payload_len, b->expected, b->capacity,
+                                      b->file_records, b->file_status, b->rewalks, stream);
+    if (rc)
+        return rc;
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    uint64_t n = 0;
+    if (nfiles) {
+        if (hipMemcpyAsync(&n, b->file_records + nfiles, sizeof(n), hipMemcpyDeviceToHost, st) != hipSuccess ||
+            hipStreamSynchronize(st) != hipSuccess)
+            return ZDB_CRC32_ELAUNCH;
+    }
+    *n_records = n;
+    if (n > b->capacity)
+        return ZDB_CRC32_ENOSPC;
+    return zdb_crc32_verify_device(d_image, b->payload_off, b->payload_len, b->expected, b->computed,
+                                   b->mismatch, b->mismatch_count, b->max_mismatch, n, stream);
+}
+
+} // extern "C"

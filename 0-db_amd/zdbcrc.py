@@ -67,6 +67,19 @@ _verify_device = _fn("zdb_crc32_verify_device", C.c_int, vp, vp, vp, vp, vp, vp,
                      C.c_size_t, vp)
 _batch_host = _fn("zdb_crc32_batch", C.c_int, vp, C.c_size_t, vp, vp, vp, C.c_size_t)
 _check_device = _fn("zdb_datafile_check_device", C.c_int, vp, C.c_uint64, vp, vp, C.c_size_t, vp)
+_walk_device = _fn("zdb_datafile_walk_device", C.c_int, vp, vp, vp, C.c_uint32, C.c_uint64, C.c_uint32, vp, vp,
+                   vp, vp, C.c_uint64, vp, vp, vp, vp)
+
+
+class ScanBuffers(C.Structure):
+    """zdb_scan_buffers_t (include/zdb_datafile.h)"""
+    _fields_ = [("entry_off", vp), ("payload_off", vp), ("payload_len", vp), ("expected", vp), ("computed", vp),
+                ("capacity", C.c_uint64), ("file_records", vp), ("file_status", vp), ("rewalks", vp),
+                ("mismatch", vp), ("mismatch_count", vp), ("max_mismatch", C.c_uint32)]
+
+
+_scan_device = _fn("zdb_datafile_scan_device", C.c_int, vp, vp, vp, C.c_uint32, C.c_uint64, C.c_uint32,
+                   C.POINTER(ScanBuffers), C.POINTER(C.c_uint64), vp)
 _host_alloc = _fn("zdb_crc32_host_alloc", vp, C.c_size_t)
 _host_free = _fn("zdb_crc32_host_free", None, vp)
 _set_timing = _fn("zdb_crc32_set_timing", None, C.c_int)
@@ -95,6 +108,7 @@ EXPORTED = [
     "zdb_crc32_kernel_stats", "zdb_synth_fill", "zdb_synth_fill_device", "zdb_synth_zipf_lengths",
     "zdb_datafile_walk", "zdb_datafile_encode_entry", "zdb_datafile_encode_header",
     "zdb_datafile_payloads", "zdb_datafile_encode_batch", "zdb_datafile_check_device",
+    "zdb_datafile_walk_device", "zdb_datafile_scan_device",
 ]
 
 RECORD_DTYPE = np.dtype([
@@ -104,7 +118,8 @@ RECORD_DTYPE = np.dtype([
 ])
 assert RECORD_DTYPE.itemsize == 40
 
-WALK_OK, WALK_SHORT_HEADER, WALK_SHORT_PAYLOAD, WALK_BAD_DESCRIPTOR = 0, 1, 2, 3
+WALK_OK, WALK_SHORT_HEADER, WALK_SHORT_PAYLOAD, WALK_BAD_DESCRIPTOR, WALK_EXCEEDS_BOUND = 0, 1, 2, 3, 4
+ENOSPC = -5
 
 
 class ZdbCrcError(RuntimeError):
@@ -210,6 +225,57 @@ def datafile_check_device(image, record_offsets, result, stream=None):
         _dev_check(t, d, nm)
     _check(_check_device(image.data_ptr(), image.numel(), record_offsets.data_ptr(), result.data_ptr(),
                          record_offsets.numel(), _stream_handle(stream)), "zdb_datafile_check_device")
+
+
+class DeviceStore:
+    """A store of datafile images in device memory (torch tensors) and the
+    buffers of a device walk / scan over it (f3: zdb_datafile_walk_device,
+    zdb_datafile_scan_device)."""
+
+    def __init__(self, image, file_off, file_len, capacity: int, max_mismatch: int = 1024):
+        import torch
+        _dev_check(image, torch.uint8, "image")
+        self.image = image
+        self.file_off = torch.as_tensor(np.asarray(file_off, np.int64)).cuda()
+        self.file_len = torch.as_tensor(np.asarray(file_len, np.int64)).cuda()
+        self.nfiles = len(file_off)
+        self.max_file_len = int(np.max(file_len)) if len(file_len) else 0
+        dv = image.device
+        self.capacity = capacity
+        self.entry_off = torch.zeros(max(capacity, 1), dtype=torch.int64, device=dv)
+        self.payload_off = torch.zeros(max(capacity, 1), dtype=torch.int64, device=dv)
+        self.payload_len = torch.zeros(max(capacity, 1), dtype=torch.int32, device=dv)
+        self.expected = torch.zeros(max(capacity, 1), dtype=torch.int32, device=dv)
+        self.computed = torch.zeros(max(capacity, 1), dtype=torch.int32, device=dv)
+        self.file_records = torch.zeros(self.nfiles + 1, dtype=torch.int64, device=dv)
+        self.file_status = torch.zeros(max(self.nfiles, 1), dtype=torch.int32, device=dv)
+        self.rewalks = torch.zeros(self.nfiles + 1, dtype=torch.int32, device=dv)
+        self.mismatch = torch.zeros(max(max_mismatch, 1), dtype=torch.int32, device=dv)
+        self.mismatch_count = torch.zeros(1, dtype=torch.int32, device=dv)
+        self.max_mismatch = max_mismatch
+        self.buffers = ScanBuffers(
+            self.entry_off.data_ptr(), self.payload_off.data_ptr(), self.payload_len.data_ptr(),
+            self.expected.data_ptr(), self.computed.data_ptr(), capacity, self.file_records.data_ptr(),
+            self.file_status.data_ptr(), self.rewalks.data_ptr(), self.mismatch.data_ptr(),
+            self.mismatch_count.data_ptr(), max_mismatch)
+
+    def walk(self, chunk_bytes: int = 0, stream=None):
+        """async: descriptors of every record, in file order"""
+        _check(_walk_device(self.image.data_ptr(), self.file_off.data_ptr(), self.file_len.data_ptr(), self.nfiles,
+                            self.max_file_len, chunk_bytes, self.entry_off.data_ptr(), self.payload_off.data_ptr(),
+                            self.payload_len.data_ptr(), self.expected.data_ptr(), self.capacity,
+                            self.file_records.data_ptr(), self.file_status.data_ptr(), self.rewalks.data_ptr(),
+                            _stream_handle(stream)), "zdb_datafile_walk_device")
+
+    def scan(self, chunk_bytes: int = 0, stream=None) -> int:
+        """walk + checksum + compare (synchronises once); returns the record count"""
+        n = C.c_uint64(0)
+        rc = _scan_device(self.image.data_ptr(), self.file_off.data_ptr(), self.file_len.data_ptr(), self.nfiles,
+                          self.max_file_len, chunk_bytes, C.byref(self.buffers), C.byref(n), _stream_handle(stream))
+        if rc == ENOSPC:
+            raise ZdbCrcError(f"zdb_datafile_scan_device: {n.value} records > capacity {self.capacity}")
+        _check(rc, "zdb_datafile_scan_device")
+        return n.value
 
 
 def verify_device(arena, offsets, lengths, expected, out, mismatch, count, stream=None):

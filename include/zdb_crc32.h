@@ -60,6 +60,7 @@ size_t zdb_crc32_table_image(uint32_t *dst, size_t dwords);
 #define ZDB_CRC32_EINVAL       -2  /* bad argument                          */
 #define ZDB_CRC32_ENOMEM       -3  /* device allocation failed              */
 #define ZDB_CRC32_ELAUNCH      -4  /* kernel launch / runtime error         */
+#define ZDB_CRC32_ENOSPC       -5  /* caller's output buffers too small     */
 
 const char *zdb_crc32_strerror(int code);
 

@@ -45,6 +45,7 @@ typedef struct zdb_record_t {
 #define ZDB_WALK_SHORT_HEADER   1  /* "data header read failed" (:68-69)              */
 #define ZDB_WALK_SHORT_PAYLOAD  2  /* "payload entry read failed" (:87-88)            */
 #define ZDB_WALK_BAD_DESCRIPTOR 3  /* short file header, magic or version (data.c:197-206) */
+#define ZDB_WALK_EXCEEDS_BOUND  4  /* device walk only: file longer than the caller's max_file_len */
 
 /* Walk the entry headers of an in-memory datafile image (the serial chain of
  * integrity-check.c:59-69 / data.c:306-311).  Fills up to max_records
@@ -95,6 +96,58 @@ size_t zdb_datafile_payloads(const zdb_record_t *recs, size_t nrecs, uint64_t *o
  * is no CPU fallback. */
 int zdb_datafile_check_device(const uint8_t *d_image, uint64_t image_len, const uint64_t *d_offsets,
                               int32_t *d_result, size_t n, void *stream);
+
+/* f3 -- record-boundary discovery on the GPU (the serial chain of
+ * integrity-check.c:59-69 / data.c:306-311, found without it): nfiles
+ * datafile images in device memory, file i at d_image + d_file_off[i] of
+ * d_file_len[i] bytes (device arrays; every file <= max_file_len <= 4 GiB,
+ * the image readable 16 bytes past each file's end).  Each file is cut into
+ * chunks of chunk_bytes (a power of two >= 1 KiB; 0 = 4 MiB) whose chains
+ * are discovered speculatively (header filter + the next entry's `previous`
+ * back-pointer) and stitched exactly from offset 28; a chunk whose guess is
+ * wrong is re-walked serially, so the result is always the serial walk's.
+ *
+ * Outputs (device, written on `stream`, asynchronous):
+ *   d_file_records[nfiles + 1]  exclusive prefix of the files' record counts
+ *                               (entry nfiles = total records);
+ *   d_file_status[nfiles]       ZDB_WALK_* of each file, as zdb_datafile_walk;
+ *   d_rewalks[nfiles + 1]       chunks re-walked serially per file (+ total);
+ *   up to `capacity` records in file order: d_entry_off (image offset of the
+ *   entry header), d_payload_off, d_payload_len and d_expected (the stored
+ *   integrity).  d_payload_len / d_expected are 0 for records the
+ *   integrity check skips (datalength 0, integrity-check.c:81-82) and for a
+ *   payload cut by the end of the file (ZDB_WALK_SHORT_PAYLOAD), so the
+ *   descriptors feed zdb_crc32_verify_device as they are. */
+int zdb_datafile_walk_device(const uint8_t *d_image, const uint64_t *d_file_off, const uint64_t *d_file_len,
+                             uint32_t nfiles, uint64_t max_file_len, uint32_t chunk_bytes, uint64_t *d_entry_off,
+                             uint64_t *d_payload_off, uint32_t *d_payload_len, uint32_t *d_expected,
+                             uint64_t capacity, uint64_t *d_file_records, int32_t *d_file_status,
+                             uint32_t *d_rewalks, void *stream);
+
+/* device buffers of a device-resident integrity scan (all device pointers) */
+typedef struct zdb_scan_buffers_t {
+    uint64_t *entry_off;      /* [capacity]                                  */
+    uint64_t *payload_off;    /* [capacity]                                  */
+    uint32_t *payload_len;    /* [capacity]                                  */
+    uint32_t *expected;       /* [capacity] stored integrity (0 if skipped)  */
+    uint32_t *computed;       /* [capacity] crc of each payload              */
+    uint64_t capacity;
+    uint64_t *file_records;   /* [nfiles + 1]                                */
+    int32_t *file_status;     /* [nfiles]                                    */
+    uint32_t *rewalks;        /* [nfiles + 1]                                */
+    uint32_t *mismatch;       /* [max_mismatch] record indices, unordered    */
+    uint32_t *mismatch_count; /* [1]                                         */
+    uint32_t max_mismatch;
+} zdb_scan_buffers_t;
+
+/* The integrity scan of a whole store, device-resident (tools/integrity-check
+ * over every file: integrity-check.c:59-105): zdb_datafile_walk_device, one
+ * synchronisation to learn the record count (*n_records), then the batched
+ * checksum + compare (zdb_crc32_verify_device) over the walked records.
+ * Returns ZDB_CRC32_ENOSPC (with *n_records set) when capacity is too small. */
+int zdb_datafile_scan_device(const uint8_t *d_image, const uint64_t *d_file_off, const uint64_t *d_file_len,
+                             uint32_t nfiles, uint64_t max_file_len, uint32_t chunk_bytes,
+                             const zdb_scan_buffers_t *buffers, uint64_t *n_records, void *stream);
 
 #ifdef __cplusplus
 }

@@ -34,8 +34,10 @@ def test_windows_cover_every_piece_bit_once():
     bits = [km.window_bit(j, t) for j in range(km.PCH) for t in range(5)]
     used = sorted(b for b in bits if b >= 0)
     assert used == list(range(128))
-    # the library's table builder uses the same map
-    f = zdbcrc._lib.zdbcrc_window_bit
+    # the library's table builder uses the same map (internal symbol: the
+    # diagnostic build exports it, the product library does not)
+    diag = ctypes.CDLL(str(zdbcrc.LIB_PATH.parent / "libzdbcrc_diag.so"))
+    f = diag.zdbcrc_window_bit
     f.restype, f.argtypes = ctypes.c_int, [ctypes.c_int, ctypes.c_int]
     assert [f(j, t) for j in range(km.PCH) for t in range(5)] == bits
 
