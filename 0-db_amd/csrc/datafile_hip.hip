@@ -60,6 +60,7 @@ constexpr uint32_t FILTER_MAX_PAYLOAD = 8u << 20; // ZDB_DATA_MAX_PAYLOAD, data.
 constexpr uint32_t FILTER_MAX_FLAGS = 3;          // DELETED | TRUNCATED, data.h:47-51 (filter only)
 constexpr uint32_t DEFAULT_LG_CHUNK = 22;         // 4 MiB
 constexpr uint32_t WALK_T = 256;
+constexpr int SU = 8; // search: KiB per wave iteration
 
 // little-endian u32 at any byte address: two aligned dword loads + one
 // v_alignbyte (reads up to 7 bytes past p; images are readable 16 bytes past
@@ -87,13 +88,27 @@ __device__ __forceinline__ int32_t hop(const uint8_t *f, uint64_t len, uint64_t 
     return ST_CONTINUE;
 }
 
-// follow the chain from pos while pos < cend; EMIT writes the records
-template <bool EMIT>
-__device__ __forceinline__ void walk_chain(const uint8_t *f, uint64_t len, uint64_t foff, uint64_t pos, uint64_t cend,
-                                           uint32_t &count, uint64_t &exit, int32_t &st, uint64_t idx,
-                                           uint64_t capacity, uint64_t *__restrict__ entry_off,
-                                           uint64_t *__restrict__ poff, uint32_t *__restrict__ plen,
-                                           uint32_t *__restrict__ expect) {
+// what a walked record turns into: image offsets of header and payload, and
+// the checksum descriptor (length and expected crc are 0 for the records the
+// integrity check skips: datalength 0, integrity-check.c:81-82, and a
+// payload cut by the end of the file)
+struct RecSlot {
+    uint32_t pos;    // file-relative header offset (datafiles are < 4 GiB)
+    uint32_t len;    // payload length to checksum
+    uint32_t expect; // stored integrity
+    uint32_t hlen;   // 18 + idlength
+};
+
+enum WalkMode { COUNT = 0, SPEC = 1, EMIT = 2 };
+
+// follow the chain from pos while pos < cend.  SPEC keeps the first kcap
+// records in the chunk's slots; EMIT writes the final descriptors at idx..
+template <int MODE>
+__device__ __forceinline__ void walk_chain(const uint8_t *f, uint64_t len, uint64_t pos, uint64_t cend,
+                                           uint32_t &count, uint64_t &exit, int32_t &st, RecSlot *slots,
+                                           uint32_t kcap, uint64_t foff, uint64_t idx, uint64_t capacity,
+                                           uint64_t *__restrict__ entry_off, uint64_t *__restrict__ poff,
+                                           uint32_t *__restrict__ plen, uint32_t *__restrict__ expect) {
     count = 0;
     st = ST_CONTINUE;
     while (pos < cend) {
@@ -108,12 +123,18 @@ __device__ __forceinline__ void walk_chain(const uint8_t *f, uint64_t len, uint6
             st = s;
             break;
         }
-        if (EMIT && idx < capacity) {
+        if (MODE != COUNT) {
             const bool full = s == ST_CONTINUE && L > 0; // payload present and non-empty
-            entry_off[idx] = foff + pos;
-            poff[idx] = foff + pos + ZDB_ENTRY_HEADER_SIZE + f[pos];
-            plen[idx] = full ? L : 0u;
-            expect[idx] = full ? ld_le32(f + pos + 9) : 0u; // empty payloads are skipped (integrity-check.c:81-82)
+            const uint32_t hlen = ZDB_ENTRY_HEADER_SIZE + f[pos];
+            const uint32_t ex = full ? ld_le32(f + pos + 9) : 0u;
+            if (MODE == SPEC && count < kcap) {
+                slots[count] = RecSlot{(uint32_t)pos, full ? L : 0u, ex, hlen};
+            } else if (MODE == EMIT && idx < capacity) {
+                entry_off[idx] = foff + pos;
+                poff[idx] = foff + pos + hlen;
+                plen[idx] = full ? L : 0u;
+                expect[idx] = ex;
+            }
         }
         idx++;
         count++;
@@ -173,15 +194,25 @@ __global__ __launch_bounds__(WALK_T) void walk_search_kernel(FileTab t, uint64_t
     } else if (c0 < len && len >= ZDB_ENTRY_HEADER_SIZE) {
         // positions p in [c0, c0 + C) with a whole 18-byte header in the file
         const uint64_t lim = (c0 + C < len - (ZDB_ENTRY_HEADER_SIZE - 1)) ? c0 + C : len - (ZDB_ENTRY_HEADER_SIZE - 1);
-        for (uint64_t b = c0; b < lim && start == NONE; b += 1024) {
-            const uint64_t p0 = b + 16u * lane; // c0 is a multiple of C >= 1 KiB: 16-byte aligned
-            uint32_t m = 0;
-            uint32_t wv[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-            if (p0 < lim) {
-                const uint4 a0 = *reinterpret_cast<const uint4 *>(f + p0);
-                const uint4 a1 = *reinterpret_cast<const uint4 *>(f + p0 + 16);
-                wv[0] = a0.x; wv[1] = a0.y; wv[2] = a0.z; wv[3] = a0.w;
-                wv[4] = a1.x; wv[5] = a1.y; wv[6] = a1.z; wv[7] = a1.w;
+        // SU KiB per iteration with every load in flight (the search is a
+        // latency chain: one round trip per iteration)
+        for (uint64_t b = c0; b < lim && start == NONE; b += 1024 * SU) {
+            uint4 a0[SU], a1[SU];
+#pragma unroll
+            for (int u = 0; u < SU; u++) {
+                const uint64_t p0 = b + 1024u * u + 16u * lane; // 16-byte aligned (c0 is a multiple of C)
+                if (p0 < lim) {
+                    a0[u] = *reinterpret_cast<const uint4 *>(f + p0);
+                    a1[u] = *reinterpret_cast<const uint4 *>(f + p0 + 16);
+                } else {
+                    a0[u] = a1[u] = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu);
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < SU; u++) {
+                const uint64_t p0 = b + 1024u * u + 16u * lane;
+                const uint32_t wv[8] = {a0[u].x, a0[u].y, a0[u].z, a0[u].w, a1[u].x, a1[u].y, a1[u].z, a1[u].w};
+                uint32_t m = 0;
 #pragma unroll
                 for (int k = 0; k < 16; k++) {
                     const int d = (k + 1) >> 2, sh = (k + 1) & 3;
@@ -189,27 +220,27 @@ __global__ __launch_bounds__(WALK_T) void walk_search_kernel(FileTab t, uint64_t
                     const uint32_t flags = (wv[(k + 13) >> 2] >> (8 * ((k + 13) & 3))) & 0xFFu;
                     m |= (uint32_t)(L <= FILTER_MAX_PAYLOAD && flags <= FILTER_MAX_FLAGS) << k;
                 }
-                const uint64_t room = lim - p0; // positions p0 + k < lim
-                if (room < 16)
-                    m &= (1u << room) - 1u;
-            }
-            uint64_t found = NONE;
-            while (m) {
-                const int k = __builtin_ctz(m);
-                m &= m - 1;
-                const int d = (k + 1) >> 2, sh = (k + 1) & 3;
-                const uint32_t L = __builtin_amdgcn_alignbyte(wv[d + 1], wv[d], (uint32_t)sh);
-                const uint32_t idl = (wv[k >> 2] >> (8 * (k & 3))) & 0xFFu;
-                if (plausible_successor(f, len, p0 + k, idl, L)) {
-                    found = p0 + k;
+                if (p0 >= lim)
+                    m = 0;
+                else if (lim - p0 < 16) // positions p0 + k < lim only
+                    m &= (1u << (lim - p0)) - 1u;
+                uint64_t found = NONE;
+                while (m) { // rare: a filter pass; confirm through the successor's back-pointer
+                    const uint32_t k = (uint32_t)__builtin_ctz(m);
+                    m &= m - 1;
+                    const uint64_t p = p0 + k;
+                    if (plausible_successor(f, len, p, f[p], ld_le32(f + p + 1))) {
+                        found = p;
+                        break;
+                    }
+                }
+                const uint64_t hit = __ballot(found != NONE);
+                if (hit) { // lanes hold increasing addresses: the lowest lane has the first candidate
+                    const uint32_t l = (uint32_t)__builtin_ctzll(hit);
+                    start = ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(found >> 32), l) << 32) |
+                            __builtin_amdgcn_readlane((uint32_t)found, l);
                     break;
                 }
-            }
-            const uint64_t hit = __ballot(found != NONE);
-            if (hit) { // lanes hold increasing addresses: the lowest lane has the first candidate
-                const uint32_t l = (uint32_t)__builtin_ctzll(hit);
-                start = ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(found >> 32), l) << 32) |
-                        __builtin_amdgcn_readlane((uint32_t)found, l);
             }
         }
     }
@@ -219,10 +250,13 @@ __global__ __launch_bounds__(WALK_T) void walk_search_kernel(FileTab t, uint64_t
     }
 }
 
-// A2: speculative chain of every chunk (one thread per chunk)
+// A2: speculative chain of every chunk (one thread per chunk, 64 chains in
+// flight per wave); the first kcap records go to the chunk's slots so that an
+// accepted chunk is emitted by a parallel copy instead of a second walk
 __global__ __launch_bounds__(WALK_T) void walk_spec_kernel(FileTab t, const uint64_t *__restrict__ s_start,
                                                            uint64_t *__restrict__ s_exit, uint32_t *__restrict__ s_count,
-                                                           int32_t *__restrict__ s_status) {
+                                                           int32_t *__restrict__ s_status, RecSlot *__restrict__ slots,
+                                                           uint32_t kcap) {
     const uint64_t w = (uint64_t)blockIdx.x * WALK_T + threadIdx.x;
     if (w >= (uint64_t)t.nfiles * t.cpf)
         return;
@@ -235,12 +269,14 @@ __global__ __launch_bounds__(WALK_T) void walk_spec_kernel(FileTab t, const uint
     uint32_t count;
     uint64_t exit;
     int32_t st;
-    walk_chain<false>(t.image + t.file_off[fi], len, 0, start, cend, count, exit, st, 0, 0, nullptr, nullptr,
-                      nullptr, nullptr);
+    walk_chain<SPEC>(t.image + t.file_off[fi], len, start, cend, count, exit, st, slots + w * kcap, kcap, 0, 0, 0,
+                     nullptr, nullptr, nullptr, nullptr);
     s_exit[w] = exit;
     s_count[w] = count;
     s_status[w] = st;
 }
+
+enum ChunkMode : uint32_t { MODE_NONE = 0, MODE_COPY = 1, MODE_WALK = 2 };
 
 // B: exact stitch (one thread per file); re-walks a chunk serially when its
 // speculative start is not the true exit of the chunk before it
@@ -250,6 +286,7 @@ __global__ __launch_bounds__(WALK_T) void walk_stitch_kernel(FileTab t, const ui
                                                              const int32_t *__restrict__ s_status,
                                                              uint64_t *__restrict__ true_start,
                                                              uint64_t *__restrict__ chunk_base,
+                                                             uint32_t *__restrict__ chunk_mode, uint32_t kcap,
                                                              uint64_t *__restrict__ file_records,
                                                              int32_t *__restrict__ file_status,
                                                              uint32_t *__restrict__ rewalks) {
@@ -276,6 +313,7 @@ __global__ __launch_bounds__(WALK_T) void walk_stitch_kernel(FileTab t, const ui
         chunk_base[w] = total;
         if (st != ST_CONTINUE || pos >= cend) { // walk over, or no record starts in this chunk
             true_start[w] = NONE;
+            chunk_mode[w] = MODE_NONE;
             continue;
         }
         true_start[w] = pos;
@@ -286,8 +324,11 @@ __global__ __launch_bounds__(WALK_T) void walk_stitch_kernel(FileTab t, const ui
             count = s_count[w];
             exit = s_exit[w];
             cs = s_status[w];
+            chunk_mode[w] = count <= kcap ? MODE_COPY : MODE_WALK;
         } else {
-            walk_chain<false>(f, len, 0, pos, cend, count, exit, cs, 0, 0, nullptr, nullptr, nullptr, nullptr);
+            walk_chain<COUNT>(f, len, pos, cend, count, exit, cs, nullptr, 0, 0, 0, 0, nullptr, nullptr, nullptr,
+                              nullptr);
+            chunk_mode[w] = MODE_WALK;
             redo++;
         }
         total += count;
@@ -317,18 +358,44 @@ __global__ void walk_prefix_kernel(uint32_t nfiles, uint64_t *__restrict__ file_
     rewalks[nfiles] = redo;
 }
 
-// C: descriptors in file order (one thread per chunk)
+// C1: descriptors of the accepted chunks, copied from their slots (one
+// thread per slot)
+__global__ __launch_bounds__(WALK_T) void walk_copy_kernel(FileTab t, const uint32_t *__restrict__ chunk_mode,
+                                                           const uint32_t *__restrict__ s_count,
+                                                           const RecSlot *__restrict__ slots, uint32_t kcap,
+                                                           const uint64_t *__restrict__ chunk_base,
+                                                           const uint64_t *__restrict__ file_base, uint64_t capacity,
+                                                           uint64_t *__restrict__ entry_off, uint64_t *__restrict__ poff,
+                                                           uint32_t *__restrict__ plen,
+                                                           uint32_t *__restrict__ expect) {
+    const uint64_t g = (uint64_t)blockIdx.x * WALK_T + threadIdx.x;
+    const uint64_t w = g / kcap;
+    const uint32_t i = (uint32_t)(g % kcap);
+    if (w >= (uint64_t)t.nfiles * t.cpf || chunk_mode[w] != MODE_COPY || i >= s_count[w])
+        return;
+    const uint32_t fi = (uint32_t)(w / t.cpf);
+    const uint64_t idx = file_base[fi] + chunk_base[w] + i;
+    if (idx >= capacity)
+        return;
+    const RecSlot r = slots[w * kcap + i];
+    const uint64_t foff = t.file_off[fi];
+    entry_off[idx] = foff + r.pos;
+    poff[idx] = foff + r.pos + r.hlen;
+    plen[idx] = r.len;
+    expect[idx] = r.expect;
+}
+
+// C2: descriptors of the chunks that had to be re-walked, or had more
+// records than slots (one thread per chunk)
 __global__ __launch_bounds__(WALK_T) void walk_emit_kernel(FileTab t, const uint64_t *__restrict__ true_start,
+                                                           const uint32_t *__restrict__ chunk_mode,
                                                            const uint64_t *__restrict__ chunk_base,
                                                            const uint64_t *__restrict__ file_base, uint64_t capacity,
                                                            uint64_t *__restrict__ entry_off, uint64_t *__restrict__ poff,
                                                            uint32_t *__restrict__ plen,
                                                            uint32_t *__restrict__ expect) {
     const uint64_t w = (uint64_t)blockIdx.x * WALK_T + threadIdx.x;
-    if (w >= (uint64_t)t.nfiles * t.cpf)
-        return;
-    const uint64_t start = true_start[w];
-    if (start == NONE)
+    if (w >= (uint64_t)t.nfiles * t.cpf || chunk_mode[w] != MODE_WALK)
         return;
     const uint32_t fi = (uint32_t)(w / t.cpf), c = (uint32_t)(w % t.cpf);
     const uint64_t cend = ((uint64_t)c + 1) << t.lg;
@@ -336,7 +403,7 @@ __global__ __launch_bounds__(WALK_T) void walk_emit_kernel(FileTab t, const uint
     uint32_t count;
     uint64_t exit;
     int32_t st;
-    walk_chain<true>(t.image + foff, t.file_len[fi], foff, start, cend, count, exit, st,
+    walk_chain<EMIT>(t.image + foff, t.file_len[fi], true_start[w], cend, count, exit, st, nullptr, 0, foff,
                      file_base[fi] + chunk_base[w], capacity, entry_off, poff, plen, expect);
 }
 
@@ -382,9 +449,10 @@ int zdb_datafile_walk_device(const uint8_t *d_image, const uint64_t *d_file_off,
     hipStream_t st = static_cast<hipStream_t>(stream);
     std::lock_guard<std::mutex> g(g_walk_mu[dev]);
     // workspace: per chunk s_start, s_exit, true_start, chunk_base (u64),
-    // s_count (u32), s_status (i32)
+    // s_count, s_status, chunk_mode (4 B), kcap record slots (16 B each)
+    const uint32_t kcap = nchunks <= 65536 ? 512u : 64u;
     auto al = [](size_t x) { return (x + 255) & ~size_t(255); };
-    const size_t need = 4 * al(nchunks * 8) + 2 * al(nchunks * 4);
+    const size_t need = 4 * al(nchunks * 8) + 3 * al(nchunks * 4) + al(nchunks * kcap * sizeof(RecSlot));
     WalkWs &ws = g_walk_ws[dev][stream];
     if (ws.bytes < need) {
         if (ws.ptr) {
@@ -404,19 +472,28 @@ int zdb_datafile_walk_device(const uint8_t *d_image, const uint64_t *d_file_off,
     uint64_t *chunk_base = reinterpret_cast<uint64_t *>(b + 3 * al(nchunks * 8));
     uint32_t *s_count = reinterpret_cast<uint32_t *>(b + 4 * al(nchunks * 8));
     int32_t *s_status = reinterpret_cast<int32_t *>(b + 4 * al(nchunks * 8) + al(nchunks * 4));
+    uint32_t *chunk_mode = reinterpret_cast<uint32_t *>(b + 4 * al(nchunks * 8) + 2 * al(nchunks * 4));
+    RecSlot *slots = reinterpret_cast<RecSlot *>(b + 4 * al(nchunks * 8) + 3 * al(nchunks * 4));
 
     const FileTab t{d_image, d_file_off, d_file_len, nfiles, (uint32_t)cpf64, lg};
     const uint32_t waves_per_block = WALK_T / 64;
     hipLaunchKernelGGL(walk_search_kernel, dim3((uint32_t)((nchunks + waves_per_block - 1) / waves_per_block)),
                        dim3(WALK_T), 0, st, t, s_start, s_status);
     const dim3 gch((uint32_t)((nchunks + WALK_T - 1) / WALK_T));
-    hipLaunchKernelGGL(walk_spec_kernel, gch, dim3(WALK_T), 0, st, t, s_start, s_exit, s_count, s_status);
+    hipLaunchKernelGGL(walk_spec_kernel, gch, dim3(WALK_T), 0, st, t, s_start, s_exit, s_count, s_status, slots,
+                       kcap);
     hipLaunchKernelGGL(walk_stitch_kernel, dim3((nfiles + WALK_T - 1) / WALK_T), dim3(WALK_T), 0, st, t, s_start,
-                       s_exit, s_count, s_status, true_start, chunk_base, d_file_records, d_file_status, d_rewalks);
+                       s_exit, s_count, s_status, true_start, chunk_base, chunk_mode, kcap, d_file_records,
+                       d_file_status, d_rewalks);
     hipLaunchKernelGGL(walk_prefix_kernel, dim3(1), dim3(64), 0, st, nfiles, d_file_records, d_rewalks);
-    if (capacity)
-        hipLaunchKernelGGL(walk_emit_kernel, gch, dim3(WALK_T), 0, st, t, true_start, chunk_base, d_file_records,
-                           capacity, d_entry_off, d_payload_off, d_payload_len, d_expected);
+    if (capacity) {
+        const uint64_t nslots = nchunks * kcap;
+        hipLaunchKernelGGL(walk_copy_kernel, dim3((uint32_t)((nslots + WALK_T - 1) / WALK_T)), dim3(WALK_T), 0, st,
+                           t, chunk_mode, s_count, slots, kcap, chunk_base, d_file_records, capacity, d_entry_off,
+                           d_payload_off, d_payload_len, d_expected);
+        hipLaunchKernelGGL(walk_emit_kernel, gch, dim3(WALK_T), 0, st, t, true_start, chunk_mode, chunk_base,
+                           d_file_records, capacity, d_entry_off, d_payload_off, d_payload_len, d_expected);
+    }
     return hipGetLastError() == hipSuccess ? ZDB_CRC32_OK : ZDB_CRC32_ELAUNCH;
 }
 
