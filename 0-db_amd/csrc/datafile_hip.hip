@@ -9,14 +9,16 @@
 // every file is cut into chunks of C bytes (default 4 MiB) and the chain is
 // discovered speculatively and stitched exactly:
 //
-//   A1 search  (one wave per chunk): the first position p >= chunk start
-//              that looks like an entry header -- datalength <= 8 MiB (the
-//              writer's cap, data.h:6), flags <= 3 (data.h:47-51) -- and whose
-//              successor q = p + 18 + idlength + datalength names p as its
-//              `previous` entry (data_insert, data.c:601), or ends the file.
-//              64 lanes x 16 positions per 1 KiB step; a random position
-//              passes the cheap filter with p ~ 2^-15 and the back-pointer
-//              check with p ~ 2^-32.
+//   A1 search  (one workgroup of 4 waves per chunk): the first position
+//              p >= chunk start that looks like an entry header -- top byte
+//              of datalength 0 (the writer caps payloads at 8 MiB, data.h:6),
+//              flags <= 3 (data.h:47-51) -- and whose successor
+//              q = p + 18 + idlength + datalength names p as its `previous`
+//              entry (data_insert, data.c:601), or ends the file.  Each wave
+//              takes 8 KiB blocks (64 lanes x 16 positions x 8, all loads in
+//              flight), one zero-byte test per 4 positions; a random position
+//              passes the filter with p ~ 2^-14 and the back-pointer check
+//              with p ~ 2^-32.
 //   A2 walk    (one thread per chunk, 64 chains in flight per wave): follow
 //              the chain from that candidate to the first header at or past
 //              the chunk end (its "exit"), counting records, stopping on the
@@ -71,14 +73,35 @@ __device__ __forceinline__ uint32_t ld_le32(const uint8_t *p) {
     return __builtin_amdgcn_alignbyte(q[1], q[0], (uint32_t)(a & 3));
 }
 
+// the fields of the entry header at pos the walk needs (data.h:56-65):
+// idlength (byte 0), datalength (1..4), integrity (9..12).  Five aligned
+// dword loads issued together -- one memory round trip per record (reads up
+// to pos + 20, within the 16 readable bytes past the file when pos + 4 <= len)
+struct Hdr {
+    uint32_t idl, L, integ;
+};
+__device__ __forceinline__ Hdr load_hdr(const uint8_t *f, uint64_t len, uint64_t pos) {
+    if (pos + 4 <= len) {
+        const uintptr_t a = reinterpret_cast<uintptr_t>(f + pos);
+        const uint32_t *q = reinterpret_cast<const uint32_t *>(a & ~uintptr_t(3));
+        const uint32_t sh = (uint32_t)(a & 3);
+        const uint32_t q0 = q[0], q1 = q[1], q2 = q[2], q3 = q[3], q4 = q[4];
+        const uint32_t w0 = __builtin_amdgcn_alignbyte(q1, q0, sh), w1 = __builtin_amdgcn_alignbyte(q2, q1, sh);
+        const uint32_t w2 = __builtin_amdgcn_alignbyte(q3, q2, sh), w3 = __builtin_amdgcn_alignbyte(q4, q3, sh);
+        return Hdr{w0 & 0xFFu, (w0 >> 8) | (w1 << 24), (w2 >> 8) | (w3 << 24)};
+    }
+    return Hdr{f[pos], 0u, 0u}; // no whole header fits: the walk stops on SHORT_HEADER
+}
+
 // one record of the serial walk at pos (datafile.c zdb_datafile_walk):
 // SHORT_HEADER -> not a record; SHORT_PAYLOAD -> a record that ends the walk
 __device__ __forceinline__ int32_t hop(const uint8_t *f, uint64_t len, uint64_t pos, uint64_t &next,
-                                       uint32_t &L) {
-    const uint64_t hlen = ZDB_ENTRY_HEADER_SIZE + (uint64_t)f[pos];
+                                       uint32_t &L, Hdr &h) {
+    h = load_hdr(f, len, pos);
+    const uint64_t hlen = ZDB_ENTRY_HEADER_SIZE + (uint64_t)h.idl;
     if (pos + hlen > len)
         return ZDB_WALK_SHORT_HEADER;
-    L = ld_le32(f + pos + 1);
+    L = h.L;
     next = pos + hlen;
     if (L) {
         if (next + L > len)
@@ -118,15 +141,16 @@ __device__ __forceinline__ void walk_chain(const uint8_t *f, uint64_t len, uint6
         }
         uint64_t next = 0;
         uint32_t L = 0;
-        const int32_t s = hop(f, len, pos, next, L);
+        Hdr h;
+        const int32_t s = hop(f, len, pos, next, L, h);
         if (s == ZDB_WALK_SHORT_HEADER) {
             st = s;
             break;
         }
         if (MODE != COUNT) {
             const bool full = s == ST_CONTINUE && L > 0; // payload present and non-empty
-            const uint32_t hlen = ZDB_ENTRY_HEADER_SIZE + f[pos];
-            const uint32_t ex = full ? ld_le32(f + pos + 9) : 0u;
+            const uint32_t hlen = ZDB_ENTRY_HEADER_SIZE + h.idl;
+            const uint32_t ex = full ? h.integ : 0u;
             if (MODE == SPEC && count < kcap) {
                 slots[count] = RecSlot{(uint32_t)pos, full ? L : 0u, ex, hlen};
             } else if (MODE == EMIT && idx < capacity) {
@@ -169,84 +193,117 @@ struct FileTab {
     uint32_t lg;  // log2 chunk bytes
 };
 
-// A1: speculative start of every chunk (one wave per chunk)
+// candidate positions among the 16 starting at a 16-byte block whose 32
+// bytes are d[0..7]: byte p+4 (top byte of datalength) is 0 and byte p+13
+// (flags) is <= 3.  One zero-byte test covers 4 positions: bit 8r+7 of z[j]
+// is set when position 4j+r qualifies (the test has no false negatives;
+// false positives only cost a back-pointer check).
+__device__ __forceinline__ uint32_t haszero(uint32_t x) { return (x - 0x01010101u) & ~x & 0x80808080u; }
+
+__device__ __forceinline__ void candidates(const uint32_t (&d)[8], uint32_t (&z)[4]) {
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        const uint32_t fl = __builtin_amdgcn_alignbyte(d[j + 4], d[j + 3], 1u); // bytes 4j+13 .. 4j+16
+        z[j] = haszero(d[j + 1]) & haszero(fl & 0xFCFCFCFCu);
+    }
+}
+
+// A1: speculative start of every chunk (one workgroup of NWS waves per chunk:
+// the waves take interleaved SU-KiB blocks, so a chunk that starts inside a
+// 1 MiB payload is searched NWS blocks at a time)
 __global__ __launch_bounds__(WALK_T) void walk_search_kernel(FileTab t, uint64_t *__restrict__ s_start,
                                                              int32_t *__restrict__ s_status) {
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint64_t w = (uint64_t)blockIdx.x * (WALK_T / 64) + (threadIdx.x >> 6);
-    if (w >= (uint64_t)t.nfiles * t.cpf)
-        return;
+    constexpr uint32_t NWS = WALK_T / 64;
+    constexpr uint64_t SB = 1024u * SU; // bytes per wave block
+    __shared__ unsigned long long best;
+    const uint32_t lane = threadIdx.x & 63u, wid = threadIdx.x >> 6;
+    const uint64_t w = blockIdx.x;
     const uint32_t fi = (uint32_t)(w / t.cpf), c = (uint32_t)(w % t.cpf);
     const uint64_t len = t.file_len[fi];
     const uint8_t *f = t.image + t.file_off[fi];
     const uint64_t C = 1ull << t.lg, c0 = (uint64_t)c * C;
-    uint64_t start = NONE;
-    int32_t st = ST_CONTINUE;
     if (c == 0) {
-        // data_descriptor_load / _validate (data.c:177-209): 28-byte header,
-        // magic "DAT0", version 3
-        const bool bad = len < ZDB_DATA_HEADER_SIZE || f[0] != 'D' || f[1] != 'A' || f[2] != 'T' ||
-                         f[3] != '0' || ld_le32(f + 4) != ZDB_DATAFILE_VERSION;
-        if (bad)
-            st = ZDB_WALK_BAD_DESCRIPTOR;
-        else
-            start = ZDB_DATA_HEADER_SIZE;
-    } else if (c0 < len && len >= ZDB_ENTRY_HEADER_SIZE) {
-        // positions p in [c0, c0 + C) with a whole 18-byte header in the file
-        const uint64_t lim = (c0 + C < len - (ZDB_ENTRY_HEADER_SIZE - 1)) ? c0 + C : len - (ZDB_ENTRY_HEADER_SIZE - 1);
-        // SU KiB per iteration with every load in flight (the search is a
-        // latency chain: one round trip per iteration)
-        for (uint64_t b = c0; b < lim && start == NONE; b += 1024 * SU) {
+        if (threadIdx.x == 0) {
+            // data_descriptor_load / _validate (data.c:177-209): 28-byte
+            // header, magic "DAT0", version 3
+            const bool bad = len < ZDB_DATA_HEADER_SIZE || f[0] != 'D' || f[1] != 'A' || f[2] != 'T' ||
+                             f[3] != '0' || ld_le32(f + 4) != ZDB_DATAFILE_VERSION;
+            s_start[w] = bad ? NONE : (uint64_t)ZDB_DATA_HEADER_SIZE;
+            s_status[w] = bad ? ZDB_WALK_BAD_DESCRIPTOR : ST_CONTINUE;
+        }
+        return;
+    }
+    if (c0 >= len || len < ZDB_ENTRY_HEADER_SIZE) {
+        if (threadIdx.x == 0) {
+            s_start[w] = NONE;
+            s_status[w] = ST_CONTINUE;
+        }
+        return;
+    }
+    // positions p in [c0, c0 + C) with a whole 18-byte header in the file
+    const uint64_t lim = (c0 + C < len - (ZDB_ENTRY_HEADER_SIZE - 1)) ? c0 + C : len - (ZDB_ENTRY_HEADER_SIZE - 1);
+    if (threadIdx.x == 0)
+        best = NONE;
+    __syncthreads();
+    for (uint64_t r0 = c0;; r0 += NWS * SB) {
+        const uint64_t b = r0 + wid * SB;
+        uint64_t found = NONE;
+        if (b < lim) {
             uint4 a0[SU], a1[SU];
 #pragma unroll
-            for (int u = 0; u < SU; u++) {
+            for (int u = 0; u < SU; u++) { // every load of the block in flight
                 const uint64_t p0 = b + 1024u * u + 16u * lane; // 16-byte aligned (c0 is a multiple of C)
                 if (p0 < lim) {
                     a0[u] = *reinterpret_cast<const uint4 *>(f + p0);
                     a1[u] = *reinterpret_cast<const uint4 *>(f + p0 + 16);
                 } else {
-                    a0[u] = a1[u] = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu);
+                    a0[u] = a1[u] = make_uint4(~0u, ~0u, ~0u, ~0u); // no candidate
                 }
             }
 #pragma unroll
             for (int u = 0; u < SU; u++) {
                 const uint64_t p0 = b + 1024u * u + 16u * lane;
-                const uint32_t wv[8] = {a0[u].x, a0[u].y, a0[u].z, a0[u].w, a1[u].x, a1[u].y, a1[u].z, a1[u].w};
-                uint32_t m = 0;
+                const uint32_t d[8] = {a0[u].x, a0[u].y, a0[u].z, a0[u].w, a1[u].x, a1[u].y, a1[u].z, a1[u].w};
+                uint32_t z[4];
+                candidates(d, z);
+                uint64_t hit = 0;
+                if (z[0] | z[1] | z[2] | z[3]) { // rare: confirm through the successor's back-pointer
 #pragma unroll
-                for (int k = 0; k < 16; k++) {
-                    const int d = (k + 1) >> 2, sh = (k + 1) & 3;
-                    const uint32_t L = __builtin_amdgcn_alignbyte(wv[d + 1], wv[d], (uint32_t)sh);
-                    const uint32_t flags = (wv[(k + 13) >> 2] >> (8 * ((k + 13) & 3))) & 0xFFu;
-                    m |= (uint32_t)(L <= FILTER_MAX_PAYLOAD && flags <= FILTER_MAX_FLAGS) << k;
-                }
-                if (p0 >= lim)
-                    m = 0;
-                else if (lim - p0 < 16) // positions p0 + k < lim only
-                    m &= (1u << (lim - p0)) - 1u;
-                uint64_t found = NONE;
-                while (m) { // rare: a filter pass; confirm through the successor's back-pointer
-                    const uint32_t k = (uint32_t)__builtin_ctz(m);
-                    m &= m - 1;
-                    const uint64_t p = p0 + k;
-                    if (plausible_successor(f, len, p, f[p], ld_le32(f + p + 1))) {
-                        found = p;
-                        break;
+                    for (int j = 0; j < 4; j++) {
+                        uint32_t m = z[j];
+                        while (m && found == NONE) {
+                            const uint32_t r = (uint32_t)__builtin_ctz(m) >> 3;
+                            m &= ~(0xFFu << (8 * r));
+                            const uint64_t p = p0 + 4u * j + r;
+                            if (p < lim) {
+                                const Hdr h = load_hdr(f, len, p);
+                                if (plausible_successor(f, len, p, h.idl, h.L))
+                                    found = p;
+                            }
+                        }
                     }
                 }
-                const uint64_t hit = __ballot(found != NONE);
-                if (hit) { // lanes hold increasing addresses: the lowest lane has the first candidate
+                hit = __ballot(found != NONE);
+                if (hit) { // lanes hold increasing addresses: the lowest lane has the block's first candidate
                     const uint32_t l = (uint32_t)__builtin_ctzll(hit);
-                    start = ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(found >> 32), l) << 32) |
+                    found = ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(found >> 32), l) << 32) |
                             __builtin_amdgcn_readlane((uint32_t)found, l);
                     break;
                 }
             }
+            if (found != NONE && lane == 0)
+                atomicMin(&best, (unsigned long long)found);
         }
-    }
-    if (lane == 0) {
-        s_start[w] = start;
-        s_status[w] = st;
+        __syncthreads();
+        const uint64_t bst = best;
+        __syncthreads();
+        if (bst != NONE || r0 + NWS * SB >= lim) { // first block with a hit found, or the chunk is done
+            if (threadIdx.x == 0) {
+                s_start[w] = bst;
+                s_status[w] = ST_CONTINUE;
+            }
+            return;
+        }
     }
 }
 
@@ -476,9 +533,7 @@ int zdb_datafile_walk_device(const uint8_t *d_image, const uint64_t *d_file_off,
     RecSlot *slots = reinterpret_cast<RecSlot *>(b + 4 * al(nchunks * 8) + 3 * al(nchunks * 4));
 
     const FileTab t{d_image, d_file_off, d_file_len, nfiles, (uint32_t)cpf64, lg};
-    const uint32_t waves_per_block = WALK_T / 64;
-    hipLaunchKernelGGL(walk_search_kernel, dim3((uint32_t)((nchunks + waves_per_block - 1) / waves_per_block)),
-                       dim3(WALK_T), 0, st, t, s_start, s_status);
+    hipLaunchKernelGGL(walk_search_kernel, dim3((uint32_t)nchunks), dim3(WALK_T), 0, st, t, s_start, s_status);
     const dim3 gch((uint32_t)((nchunks + WALK_T - 1) / WALK_T));
     hipLaunchKernelGGL(walk_spec_kernel, gch, dim3(WALK_T), 0, st, t, s_start, s_exit, s_count, s_status, slots,
                        kcap);

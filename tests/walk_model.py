@@ -73,7 +73,9 @@ def search(f, ln, c0, C):
     lim = min(c0 + C, ln - 17)
     for p in range(c0, lim):
         L = _le32(f, p + 1)
-        if L <= MAXL and _byte(f, p + 13) <= MAXF and plausible_successor(f, ln, p, int(f[p]), L):
+        # filter: top byte of datalength 0 (L < 16 MiB; the writer caps at
+        # 8 MiB, data.h:6) and flags <= 3 (data.h:47-51)
+        if _byte(f, p + 4) == 0 and _byte(f, p + 13) <= MAXF and plausible_successor(f, ln, p, int(f[p]), L):
             return p
     return NONE
 
