@@ -6,7 +6,7 @@
 // the next offset, pos' = pos + 18 + idlength + datalength
 // (integrity-check.c:59-69, data.c:306-311; host form: datafile.c).  A GPU
 // cannot follow one chain fast (one dependent HBM round trip per record), so
-// every file is cut into chunks of C bytes (default 4 MiB) and the chain is
+// every file is cut into chunks of C bytes (default 8 MiB) and the chain is
 // discovered speculatively and stitched exactly:
 //
 //   A1 search  (one workgroup of 4 waves per chunk): the first position
@@ -58,9 +58,11 @@ namespace {
 
 constexpr uint64_t NONE = ~0ull;
 constexpr int32_t ST_CONTINUE = -1;
-constexpr uint32_t FILTER_MAX_PAYLOAD = 8u << 20; // ZDB_DATA_MAX_PAYLOAD, data.h:6 (filter only)
-constexpr uint32_t FILTER_MAX_FLAGS = 3;          // DELETED | TRUNCATED, data.h:47-51 (filter only)
-constexpr uint32_t DEFAULT_LG_CHUNK = 22;         // 4 MiB
+// 8 MiB chunks: C4 (64 x 256 MiB files of C3 payloads) walks in 0.83 ms
+// against 0.91 (4 MiB), 1.28 (2 MiB) and 1.24 ms (16 MiB) --
+// profiles/r2/walk_probe.jsonl; smaller chunks search more, larger ones
+// follow longer chains
+constexpr uint32_t DEFAULT_LG_CHUNK = 23;
 constexpr uint32_t WALK_T = 256;
 constexpr int SU = 8; // search: KiB per wave iteration
 

@@ -102,7 +102,7 @@ int zdb_datafile_check_device(const uint8_t *d_image, uint64_t image_len, const 
  * datafile images in device memory, file i at d_image + d_file_off[i] of
  * d_file_len[i] bytes (device arrays; every file <= max_file_len <= 4 GiB,
  * the image readable 16 bytes past each file's end).  Each file is cut into
- * chunks of chunk_bytes (a power of two >= 1 KiB; 0 = 4 MiB) whose chains
+ * chunks of chunk_bytes (a power of two >= 1 KiB; 0 = 8 MiB) whose chains
  * are discovered speculatively (header filter + the next entry's `previous`
  * back-pointer) and stitched exactly from offset 28; a chunk whose guess is
  * wrong is re-walked serially, so the result is always the serial walk's.
