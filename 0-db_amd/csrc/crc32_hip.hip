@@ -1697,6 +1697,180 @@ int zdb_crc32_kernel_stats(double *total_ms, uint64_t *launches) {
     return ZDB_CRC32_OK;
 }
 
+// ---------------------------------------------------------------------------
+// f1: host -> device ingest stream (include/zdb_crc32.h, section 2b)
+// ---------------------------------------------------------------------------
+
+struct zdb_crc32_stream_t {
+    int dev = -1;
+    hipStream_t st = nullptr;
+    uint8_t *d_image = nullptr; // device image of the current file
+    size_t d_cap = 0, cap = 0, fill = 0;
+    size_t slot_bytes = 0;
+    int nslots = 0, next = 0;
+    uint8_t *slot[ZDB_CRC32_STREAM_MAX_SLOTS] = {};
+    hipEvent_t done[ZDB_CRC32_STREAM_MAX_SLOTS] = {};
+    bool used[ZDB_CRC32_STREAM_MAX_SLOTS] = {};
+    uint8_t *d_desc = nullptr, *h_desc = nullptr; // offsets (8 n) | lengths (4 n) | out (4 n)
+    size_t desc_cap = 0;
+};
+
+static void stream_free(zdb_crc32_stream_t *s) {
+    if (!s)
+        return;
+    if (s->dev >= 0)
+        hipSetDevice(s->dev);
+    if (s->st)
+        hipStreamSynchronize(s->st);
+    for (int i = 0; i < s->nslots; i++) {
+        if (s->slot[i])
+            hipHostFree(s->slot[i]);
+        if (s->done[i])
+            hipEventDestroy(s->done[i]);
+    }
+    if (s->d_image)
+        hipFree(s->d_image);
+    if (s->d_desc)
+        hipFree(s->d_desc);
+    if (s->h_desc)
+        hipHostFree(s->h_desc);
+    if (s->st) {
+        std::lock_guard<std::mutex> g(g_dev_mu[s->dev]);
+        auto it = g_dev[s->dev].ws.find(reinterpret_cast<void *>(s->st));
+        if (it != g_dev[s->dev].ws.end()) {
+            hipFree(it->second.ptr);
+            g_dev[s->dev].ws.erase(it);
+        }
+        hipStreamDestroy(s->st);
+    }
+    delete s;
+}
+
+zdb_crc32_stream_t *zdb_crc32_stream_open(size_t slot_bytes, int slots) {
+    if (slot_bytes < 4096 || slots < 2 || slots > ZDB_CRC32_STREAM_MAX_SLOTS)
+        return nullptr;
+    int dev;
+    if (current_device(&dev))
+        return nullptr;
+    {
+        std::lock_guard<std::mutex> g(g_dev_mu[dev]);
+        DeviceCtx *c;
+        if (ensure_device(dev, &c))
+            return nullptr;
+    }
+    zdb_crc32_stream_t *s = new zdb_crc32_stream_t;
+    s->dev = dev;
+    s->slot_bytes = slot_bytes;
+    s->nslots = slots;
+    bool ok = hipStreamCreateWithFlags(&s->st, hipStreamNonBlocking) == hipSuccess;
+    for (int i = 0; ok && i < slots; i++)
+        ok = hipHostMalloc(reinterpret_cast<void **>(&s->slot[i]), slot_bytes, hipHostMallocDefault) == hipSuccess &&
+             hipEventCreateWithFlags(&s->done[i], hipEventDisableTiming) == hipSuccess;
+    if (!ok) {
+        stream_free(s);
+        return nullptr;
+    }
+    return s;
+}
+
+int zdb_crc32_stream_begin(zdb_crc32_stream_t *s, size_t image_bytes) {
+    if (!s)
+        return ZDB_CRC32_EINVAL;
+    if (hipSetDevice(s->dev) != hipSuccess || hipStreamSynchronize(s->st) != hipSuccess)
+        return ZDB_CRC32_ELAUNCH;
+    const size_t need = image_bytes + 16; // the kernel may read up to the next 16-byte boundary
+    if (s->d_cap < need) {
+        if (s->d_image)
+            hipFree(s->d_image);
+        s->d_image = nullptr;
+        s->d_cap = 0;
+        const size_t cap = need + (need >> 3);
+        if (hipMalloc(reinterpret_cast<void **>(&s->d_image), cap) != hipSuccess)
+            return ZDB_CRC32_ENOMEM;
+        s->d_cap = cap;
+    }
+    s->cap = image_bytes;
+    s->fill = 0;
+    return ZDB_CRC32_OK;
+}
+
+int zdb_crc32_stream_append(zdb_crc32_stream_t *s, const uint8_t *src, size_t n) {
+    if (!s || (n && !src) || n > s->cap - s->fill)
+        return ZDB_CRC32_EINVAL;
+    if (hipSetDevice(s->dev) != hipSuccess)
+        return ZDB_CRC32_ELAUNCH;
+    while (n) {
+        const int i = s->next;
+        // the slot is free again once its previous copy has left it
+        if (s->used[i] && hipEventSynchronize(s->done[i]) != hipSuccess)
+            return ZDB_CRC32_ELAUNCH;
+        const size_t k = n < s->slot_bytes ? n : s->slot_bytes;
+        std::memcpy(s->slot[i], src, k);
+        if (hipMemcpyAsync(s->d_image + s->fill, s->slot[i], k, hipMemcpyHostToDevice, s->st) != hipSuccess ||
+            hipEventRecord(s->done[i], s->st) != hipSuccess)
+            return ZDB_CRC32_ELAUNCH;
+        s->used[i] = true;
+        s->fill += k;
+        src += k;
+        n -= k;
+        s->next = (i + 1) % s->nslots;
+    }
+    return ZDB_CRC32_OK;
+}
+
+int zdb_crc32_stream_checksum(zdb_crc32_stream_t *s, const uint64_t *offsets, const uint32_t *lengths,
+                              uint32_t *out, size_t n) {
+    if (!s)
+        return ZDB_CRC32_EINVAL;
+    if (n == 0)
+        return ZDB_CRC32_OK;
+    if (!offsets || !lengths || !out)
+        return ZDB_CRC32_EINVAL;
+    for (size_t r = 0; r < n; r++) // overflow-safe bounds against the appended bytes
+        if (offsets[r] > s->fill || lengths[r] > s->fill - offsets[r])
+            return ZDB_CRC32_EINVAL;
+    if (hipSetDevice(s->dev) != hipSuccess)
+        return ZDB_CRC32_ELAUNCH;
+    const size_t need = n * 16 + 64;
+    if (s->desc_cap < need) {
+        if (hipStreamSynchronize(s->st) != hipSuccess)
+            return ZDB_CRC32_ELAUNCH;
+        if (s->d_desc)
+            hipFree(s->d_desc);
+        if (s->h_desc)
+            hipHostFree(s->h_desc);
+        s->d_desc = s->h_desc = nullptr;
+        s->desc_cap = 0;
+        const size_t cap = need + (need >> 2);
+        if (hipMalloc(reinterpret_cast<void **>(&s->d_desc), cap) != hipSuccess ||
+            hipHostMalloc(reinterpret_cast<void **>(&s->h_desc), cap, hipHostMallocDefault) != hipSuccess)
+            return ZDB_CRC32_ENOMEM;
+        s->desc_cap = cap;
+    }
+    std::memcpy(s->h_desc, offsets, n * 8);
+    std::memcpy(s->h_desc + n * 8, lengths, n * 4);
+    if (hipMemcpyAsync(s->d_desc, s->h_desc, n * 12, hipMemcpyHostToDevice, s->st) != hipSuccess)
+        return ZDB_CRC32_ELAUNCH;
+    uint32_t *d_out = reinterpret_cast<uint32_t *>(s->d_desc + n * 12);
+    {
+        std::lock_guard<std::mutex> g(g_dev_mu[s->dev]);
+        DeviceCtx *c;
+        int rc = ensure_device(s->dev, &c);
+        if (!rc)
+            rc = enqueue_batch(s->dev, *c, variant(), s->d_image, reinterpret_cast<const uint64_t *>(s->d_desc),
+                               reinterpret_cast<const uint32_t *>(s->d_desc + n * 8), d_out, n, s->st);
+        if (rc)
+            return rc;
+    }
+    if (hipMemcpyAsync(s->h_desc + n * 12, d_out, n * 4, hipMemcpyDeviceToHost, s->st) != hipSuccess ||
+        hipStreamSynchronize(s->st) != hipSuccess)
+        return ZDB_CRC32_ELAUNCH;
+    std::memcpy(out, s->h_desc + n * 12, n * 4);
+    return ZDB_CRC32_OK;
+}
+
+void zdb_crc32_stream_close(zdb_crc32_stream_t *s) { stream_free(s); }
+
 int zdb_synth_fill_device(uint8_t *d_buf, size_t len, uint64_t seed, void *stream) {
     if (!len)
         return ZDB_CRC32_OK;

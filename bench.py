@@ -381,6 +381,8 @@ def e2e_legs(offs, lens, seed) -> dict:
             f.write(zdbcrc.encode_header(0) + body)
         os.symlink("d0", f"{td}/zdb-data-0")
         tools = {"gpu_tool": [str(ROOT / "0-db_amd/bin/zdb-integrity-check"), f"{td}/zdb-data-0"],
+                 "auto_engine_tool": [str(ROOT / "0-db_amd/bin/zdb-integrity-check"), "--engine=auto",
+                                      f"{td}/zdb-data-0"],
                  "scalar_engine_tool": [str(ROOT / "0-db_amd/bin/zdb-integrity-check"), "--engine=cpu",
                                         f"{td}/zdb-data-0"]}
         if oracle.REF_INTEGRITY.exists():
@@ -407,11 +409,15 @@ def e2e_legs(offs, lens, seed) -> dict:
             files.append(f"{d}/zdb-data-0")
         tool = str(ROOT / "0-db_amd/bin/zdb-integrity-check")
         scan = {"files": len(files), "file_bytes": 28 + len(body)}
-        runs = {"gpu_tool_jobs8": [[tool, "--jobs=8"] + files],
-                "scalar_engine_tool_jobs8": [[tool, "--engine=cpu", "--jobs=8"] + files]}
+        files32 = files * 4  # 32 files: a store large enough for the GPU start-up to pay off
+        runs = {"gpu_tool_jobs8": ([[tool, "--jobs=8"] + files], 8),
+                "auto_engine_tool_jobs8": ([[tool, "--engine=auto", "--jobs=8"] + files], 8),
+                "scalar_engine_tool_jobs8": ([[tool, "--engine=cpu", "--jobs=8"] + files], 8),
+                "gpu_tool_jobs8_32files": ([[tool, "--jobs=8"] + files32], 32),
+                "scalar_engine_tool_jobs8_32files": ([[tool, "--engine=cpu", "--jobs=8"] + files32], 32)}
         if oracle.REF_INTEGRITY.exists():
-            runs["reference_tool_per_file"] = [[str(oracle.REF_INTEGRITY), f] for f in files]
-        for name, cmds in runs.items():
+            runs["reference_tool_per_file"] = ([[str(oracle.REF_INTEGRITY), f] for f in files], 8)
+        for name, (cmds, nf) in runs.items():
             ts = []
             for _ in range(3):
                 t0 = time.perf_counter()
@@ -420,7 +426,11 @@ def e2e_legs(offs, lens, seed) -> dict:
                     assert p.returncode == 0, (name, p.stderr[-500:])
                 ts.append(time.perf_counter() - t0)
             scan[name + "_s"] = round(min(ts), 4)
-            scan[name + "_gibs"] = round(len(files) * (28 + len(body)) / min(ts) / GIB, 2)
+            scan[name + "_gibs"] = round(nf * (28 + len(body)) / min(ts) / GIB, 2)
+        # where the time goes in one GPU-engine run (ZDBCRC_TOOL_TRACE)
+        p = subprocess.run([tool, "--jobs=8"] + files, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE,
+                           env=dict(os.environ, ZDBCRC_TOOL_TRACE="1"), timeout=300)
+        scan["gpu_tool_trace"] = [ln for ln in p.stderr.decode().splitlines() if ln.startswith("[trace]")][:8]
         res["integrity_scan_8x256MiB"] = scan
     return res
 

@@ -97,6 +97,35 @@ int zdb_crc32_verify_device(const uint8_t *d_arena, const uint64_t *d_offsets,
 int zdb_crc32_batch(const uint8_t *arena, size_t arena_len, const uint64_t *offsets,
                     const uint32_t *lengths, uint32_t *out, size_t n);
 
+/* ------------------------------------------------------------------------
+ * 2b. Host -> device ingest stream (f1: datafiles on disk).
+ *     A device image filled chunk by chunk through a ring of pinned staging
+ *     slots: each append copies into the next free slot and queues its H2D
+ *     copy, so the caller's next read overlaps the previous transfer; then
+ *     one batched checksum over the image.  One stream per host thread, on
+ *     the device current at open.
+ * ------------------------------------------------------------------------ */
+#define ZDB_CRC32_STREAM_MAX_SLOTS 8
+
+typedef struct zdb_crc32_stream_t zdb_crc32_stream_t;
+
+/* NULL on failure (no device, bad arguments: 4 KiB <= slot_bytes, 2 <= slots
+ * <= ZDB_CRC32_STREAM_MAX_SLOTS) */
+zdb_crc32_stream_t *zdb_crc32_stream_open(size_t slot_bytes, int slots);
+
+/* start a new image of image_bytes (waits for the previous one's copies) */
+int zdb_crc32_stream_begin(zdb_crc32_stream_t *s, size_t image_bytes);
+
+/* append n bytes at the end of the image (EINVAL past image_bytes) */
+int zdb_crc32_stream_append(zdb_crc32_stream_t *s, const uint8_t *src, size_t n);
+
+/* out[r] = zdb_crc32(image + offsets[r], lengths[r]) over the bytes appended
+ * so far (EINVAL for a record past them); synchronous */
+int zdb_crc32_stream_checksum(zdb_crc32_stream_t *s, const uint64_t *offsets, const uint32_t *lengths,
+                              uint32_t *out, size_t n);
+
+void zdb_crc32_stream_close(zdb_crc32_stream_t *s);
+
 /* Number of usable HIP devices (initialises HIP; 0 when there is none). */
 int zdb_crc32_device_count(void);
 

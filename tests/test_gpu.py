@@ -266,17 +266,56 @@ def test_tail_pool_batches(dev, oracle_c):
 # ------------------------------------------------------ integrity tool ------
 
 TOOL_CASES = ["mixed", "zipf_small", "fixed_4k", "corrupt_payload", "corrupt_crc", "multi_errors",
-              "truncated_payload", "truncated_header", "bad_magic", "header_only"]
+              "truncated_payload", "truncated_header", "bad_magic", "bad_version", "header_only"]
 
 
+@pytest.mark.parametrize("engine", ["hip", "auto"])
 @pytest.mark.parametrize("name", TOOL_CASES)
-def test_tool_gpu_engine_matches_reference(tmp_path, datafile_cases, name):
+def test_tool_gpu_engine_matches_reference(tmp_path, datafile_cases, name, engine):
     from test_tool_cpu import expected, run_tool
-    out, err, code = run_tool(name, tmp_path, "hip")
+    out, err, code = run_tool(name, tmp_path, engine)
     eout, eerr = expected(name)
     assert out == eout
     assert err == eerr
     assert code == {c["name"]: c for c in datafile_cases}[name]["exit"]
+
+
+@pytest.fixture(scope="module")
+def big_datafile(tmp_path_factory):
+    """a 256 MiB datafile (65,000 x 4 KiB values) written through
+    the reference libzdb (oracle/_ref/gen_datafile_ref), three payload bytes
+    flipped, and the reference integrity-check's output on it"""
+    if not (oracle.REF_GEN.exists() and oracle.REF_INTEGRITY.exists()):
+        pytest.skip("oracle/_ref not built")
+    d = tmp_path_factory.mktemp("big")
+    subprocess.run([str(oracle.REF_GEN), str(d), "fixed", "65000", "99", "4096"], check=True, capture_output=True)
+    d0 = d / "data" / "default" / "d0"
+    img = bytearray(d0.read_bytes())
+    import zdbcrc
+    recs, _ = zdbcrc.datafile_walk(bytes(img))
+    for k in (17, 30_000, 64_999):
+        img[int(recs["payload_offset"][k]) + 100] ^= 0x21
+    d0.write_bytes(bytes(img))
+    os.symlink("d0", d / "data" / "default" / "zdb-data-0")
+    p = subprocess.run([str(oracle.REF_INTEGRITY), str(d / "data" / "default" / "zdb-data-0")], capture_output=True,
+                       env=dict(os.environ, TZ="UTC"), timeout=120)
+    assert p.returncode == 3
+    return d / "data" / "default" / "zdb-data-0", p
+
+
+@pytest.mark.parametrize("engine", ["hip", "auto"])
+def test_tool_gpu_256MiB_matches_reference(big_datafile, engine):
+    """the GPU tool on a reference-written 256 MiB datafile (three corrupt
+    payloads): stdout, stderr and exit status of the reference tool"""
+    import re
+    path, ref = big_datafile
+    from test_tool_cpu import TOOL
+    p = subprocess.run([str(TOOL), f"--engine={engine}", str(path)], capture_output=True,
+                       env=dict(os.environ, TZ="UTC"), timeout=120)
+    t = re.compile(rb"\[\s*\d+\.\d{6}\]")
+    assert p.returncode == ref.returncode == 3
+    assert t.sub(b"[T]", p.stdout) == t.sub(b"[T]", ref.stdout)
+    assert p.stderr == ref.stderr
 
 
 @pytest.mark.parametrize("jobs", [1, 3])

@@ -14,7 +14,7 @@ from pathlib import Path
 
 import pytest
 
-from conftest import GOLDEN
+from conftest import GOLDEN, ROOT
 from test_tool_cpu import TIMELOG, TOOL, expected
 
 MULTI = ["mixed", "corrupt_payload", "zipf_small", "multi_errors", "bad_magic", "fixed_4k", "header_only",
@@ -81,6 +81,55 @@ def test_fatal_file_ends_the_run(tmp_path, fatal):
     assert out == "".join(expected(n)[0] for n in names[:3])
     assert err == "".join(expected(n)[1] for n in names[:3])
     assert code == 1
+
+
+def test_auto_engine_without_gpu_is_the_reference(tmp_path, datafile_cases):
+    """--engine=auto on a machine without a GPU: every file on the scalar
+    engine, reports byte-identical to the reference's"""
+    check_multi(MULTI, tmp_path, "auto", datafile_cases, ["--jobs=3"])
+
+
+def _stub_lib(tmp: Path) -> Path:
+    src = ROOT / "0-db_amd" / "csrc"
+    so = tmp / "libzdbcrc_stub.so"
+    subprocess.run(["gcc", "-O2", "-fPIC", "-shared", "-std=gnu11", "-msse4.2", "-I", str(ROOT / "include"), "-I",
+                    str(src), "-o", str(so), str(ROOT / "tests" / "stub_libzdbcrc.c"), str(src / "crc32_cpu.c"),
+                    str(src / "crc32c_gf2.c"), "-lpthread"], check=True)
+    return so
+
+
+@pytest.mark.parametrize("jobs,gpus,devices", [(4, 3, 8), (5, 0, 2), (3, 8, 8)])
+def test_worker_to_device_mapping(tmp_path, datafile_cases, jobs, gpus, devices):
+    """--jobs=J --gpus=G over a stand-in GPU library (tests/stub_libzdbcrc.c,
+    CPU only): worker j binds device j mod min(G, devices) once, every file's
+    checksum runs on its worker's device through the ingest stream, and the
+    reports are the reference's"""
+    so = _stub_lib(tmp_path)
+    log = tmp_path / "stub.log"
+    names = ["mixed", "zipf_small", "multi_errors", "fixed_4k", "corrupt_crc", "mixed", "zipf_small", "fixed_4k"]
+    extra = [f"--jobs={jobs}"] + ([f"--gpus={gpus}"] if gpus else [])
+    fdir = tmp_path / "files"
+    fdir.mkdir()
+    dirs = stage(names, fdir)
+    env = dict(os.environ, TZ="UTC", ZDBCRC_LIB=str(so), ZDBCRC_STUB_DEVICES=str(devices), ZDBCRC_STUB_LOG=str(log))
+    p = subprocess.run([str(TOOL), "--engine=hip", *extra] + [str(d / "zdb-data-0") for d in dirs],
+                       capture_output=True, env=env, timeout=300)
+    out, err = p.stdout.decode(), p.stderr.decode()
+    for d in dirs:
+        out, err = out.replace(str(d), "@DIR@"), err.replace(str(d), "@DIR@")
+    assert TIMELOG.sub("[T]", out) == "".join(expected(n)[0] for n in names)
+    assert TIMELOG.sub("[T]", err) == "".join(expected(n)[1] for n in names)
+    exits = {c["name"]: c["exit"] for c in datafile_cases}
+    assert p.returncode == sum(exits[n] for n in names)
+    ndev = min(gpus, devices) if gpus else devices
+    lines = [ln.split() for ln in log.read_text().splitlines()]
+    # the start-up thread warms every device the workers use, in order
+    warm = [int(ln[1]) for ln in lines if ln[0] == "bind"][:ndev]
+    assert warm == list(range(ndev))
+    opened = [int(ln[1]) for ln in lines if ln[0] == "open"]  # one stream per worker that got a file
+    assert 1 <= len(opened) <= jobs and set(opened) <= {j % ndev for j in range(jobs)}
+    summed = [int(ln[1]) for ln in lines if ln[0] == "checksum"]
+    assert len(summed) == len(names) and set(summed) <= set(range(ndev))
 
 
 def test_bad_option_is_usage_error(tmp_path):
