@@ -541,6 +541,8 @@ __device__ __forceinline__ uint64_t block_excl_scan64(uint64_t v, uint64_t *wsum
 // NOZ: timing diagnostic only (skips the trailing-pad shift: wrong checksums)
 // NTL: payload loads carry the nontemporal hint (read once, never reused)
 // NOLOAD: timing diagnostic only (no payload loads: the compute floor; wrong checksums)
+// PP: the loop is unrolled twice and the two load buffers swap roles instead
+// of being copied (16 v_mov per superstep)
 // DYN > 0: tail pool.  Static slices cover the first (16 - DYN)/16 of the unit
 // space; the rest is split into DYN_POOLS pools (pool = blockIdx mod DYN_POOLS) of
 // CPW chunks per wave, claimed with one atomicAdd each as waves run out of
@@ -549,7 +551,7 @@ __device__ __forceinline__ uint64_t block_excl_scan64(uint64_t v, uint64_t *wsum
 // are flushed with atomic XOR at each claim (at most 2 are pending then).
 template <int WGT, int WPE, bool STAMP = false, int PRIO = 0, uint32_t UO = UNIT_OVH, bool NOZ = false,
           bool NTL = false, bool NOLOAD = false, int XM = 0, int DYN = 0, int CPW = 4, uint32_t DYN_POOLS = 8,
-          bool SP = false>
+          bool SP = false, bool PP = false>
 __global__ __launch_bounds__(WGT, WPE) void crc_batch_kernel_v3(
     const uint8_t *__restrict__ arena, const uint64_t *__restrict__ offsets,
     const uint32_t *__restrict__ lengths, const PlanArgs plan, uint64_t n,
@@ -708,84 +710,109 @@ __global__ __launch_bounds__(WGT, WPE) void crc_batch_kernel_v3(
 
     uint32_t *const dummy = scratch + gw;
     uint32_t css = 0, acc = 0, iter = 0;
-    for (;;) {
-        if (PRIO && (++iter & 1) == 0) {
-            const uint32_t mine = (uint32_t)(pbase + cur.us + cur.c.pa + 64u * K * css - ub);
-            if (lane == 0)
-                prog[wid] = mine;
-            const uint32_t other = lane < (uint32_t)(WGT / 64) ? prog[lane] : 0u;
-            const uint32_t ahead = (uint32_t)__popcll(__ballot(other > mine));
-            const bool slow = ahead >= (uint32_t)(WGT / 128);
-            if (PRIO == 1) {
-                if (slow)
-                    __builtin_amdgcn_s_setprio(3);
-                else
-                    __builtin_amdgcn_s_setprio(0);
-            } else if (PRIO == 2) { // older {0, 2}, younger {1, 3}
-                if (slow) {
-                    if (young)
-                        __builtin_amdgcn_s_setprio(3);
-                    else
-                        __builtin_amdgcn_s_setprio(2);
-                } else {
-                    if (young)
-                        __builtin_amdgcn_s_setprio(1);
-                    else
-                        __builtin_amdgcn_s_setprio(0);
-                }
-            } else { // older {0, 1}, younger {2, 3}
-                if (young) {
-                    if (slow)
-                        __builtin_amdgcn_s_setprio(3);
-                    else
-                        __builtin_amdgcn_s_setprio(2);
-                } else {
-                    if (slow)
-                        __builtin_amdgcn_s_setprio(1);
-                    else
-                        __builtin_amdgcn_s_setprio(0);
-                }
-            }
-        }
-        uint32_t nss = 0;
-        bool more = true;
-        if (css + 1 < cur.S) {
-            nx = cur;
-            nss = css + 1;
-        } else if (!next_seg_batched<UO>(rn, n, ub, ue, lane, m, unit_start, arena, offsets, lengths, nx) &&
-                   !(DYN && dyn && claim(nx))) {
-            more = false;
-            nx = cur;
-            nss = css;
-        }
-        load_superstep_v3<NTL, NOLOAD>(nx.c, nss, lane, bufn);
-        if (css == 0 || css + 1 == cur.S)
-            acc = superstep<true, XM>(cur.c, acc, bufc, css, cur.t0, lane, lds);
-        else
-            acc = superstep<false, XM>(cur.c, acc, bufc, css, cur.t0, lane, lds);
-        uint32_t *dst = dummy;
-        uint32_t x = 0;
-        if (css + 1 == cur.S) {
-            x = seg_value_v3<NOZ>(cur, acc, lane, lds, tables);
-            acc = 0;
-            if (cur.c.pa == 0 && cur.pb == cur.c.np) {
-                dst = out + cur.r;
-            } else {
-                cut_r[ncut & 1] = cur.r;
-                cut_x[ncut & 1] = x;
-                ncut++;
-            }
-        }
-        if (lane == 0)
+    // one superstep of the current segment (the loads of the next one are
+    // issued first); leaves `more` false once the wave's work is done
+#define ZDBCRC_STEP(BUFC, BUFN)                                                                               \
+        if (PRIO && (++iter & 1) == 0) {                                                                      \
+            const uint32_t mine = (uint32_t)(pbase + cur.us + cur.c.pa + 64u * K * css - ub);                 \
+            if (lane == 0)                                                                                    \
+                prog[wid] = mine;                                                                             \
+            const uint32_t other = lane < (uint32_t)(WGT / 64) ? prog[lane] : 0u;                             \
+            const uint32_t ahead = (uint32_t)__popcll(__ballot(other > mine));                                \
+            const bool slow = ahead >= (uint32_t)(WGT / 128);                                                 \
+            if (PRIO == 1) {                                                                                  \
+                if (slow)                                                                                     \
+                    __builtin_amdgcn_s_setprio(3);                                                            \
+                else                                                                                          \
+                    __builtin_amdgcn_s_setprio(0);                                                            \
+            } else if (PRIO == 2) {                                                                           \
+                if (slow) {                                                                                   \
+                    if (young)                                                                                \
+                        __builtin_amdgcn_s_setprio(3);                                                        \
+                    else                                                                                      \
+                        __builtin_amdgcn_s_setprio(2);                                                        \
+                } else {                                                                                      \
+                    if (young)                                                                                \
+                        __builtin_amdgcn_s_setprio(1);                                                        \
+                    else                                                                                      \
+                        __builtin_amdgcn_s_setprio(0);                                                        \
+                }                                                                                             \
+            } else {                                                                                          \
+                if (young) {                                                                                  \
+                    if (slow)                                                                                 \
+                        __builtin_amdgcn_s_setprio(3);                                                        \
+                    else                                                                                      \
+                        __builtin_amdgcn_s_setprio(2);                                                        \
+                } else {                                                                                      \
+                    if (slow)                                                                                 \
+                        __builtin_amdgcn_s_setprio(1);                                                        \
+                    else                                                                                      \
+                        __builtin_amdgcn_s_setprio(0);                                                        \
+                }                                                                                             \
+            }                                                                                                 \
+        }                                                                                                     \
+        uint32_t nss = 0;                                                                                     \
+        bool more = true;                                                                                     \
+        if (css + 1 < cur.S) {                                                                                \
+            nx = cur;                                                                                         \
+            nss = css + 1;                                                                                    \
+        } else if (!next_seg_batched<UO>(rn, n, ub, ue, lane, m, unit_start, arena, offsets, lengths, nx) &&  \
+                   !(DYN && dyn && claim(nx))) {                                                              \
+            more = false;                                                                                     \
+            nx = cur;                                                                                         \
+            nss = css;                                                                                        \
+        }                                                                                                     \
+        load_superstep_v3<NTL, NOLOAD>(nx.c, nss, lane, BUFN);                                                \
+        if (css == 0 || css + 1 == cur.S)                                                                     \
+            acc = superstep<true, XM>(cur.c, acc, BUFC, css, cur.t0, lane, lds);                              \
+        else                                                                                                  \
+            acc = superstep<false, XM>(cur.c, acc, BUFC, css, cur.t0, lane, lds);                             \
+        uint32_t *dst = dummy;                                                                                \
+        uint32_t x = 0;                                                                                       \
+        if (css + 1 == cur.S) {                                                                               \
+            x = seg_value_v3<NOZ>(cur, acc, lane, lds, tables);                                               \
+            acc = 0;                                                                                          \
+            if (cur.c.pa == 0 && cur.pb == cur.c.np) {                                                        \
+                dst = out + cur.r;                                                                            \
+            } else {                                                                                          \
+                cut_r[ncut & 1] = cur.r;                                                                      \
+                cut_x[ncut & 1] = x;                                                                          \
+                ncut++;                                                                                       \
+            }                                                                                                 \
+        }                                                                                                     \
+        if (lane == 0)                                                                                        \
             *dst = x;
-        if (!more)
-            break;
-        cur = nx;
-        css = nss;
+
+    if (PP) { // ping-pong: the two load buffers swap roles, no register copies
+        for (;;) {
+            {
+                ZDBCRC_STEP(bufc, bufn)
+                if (!more)
+                    break;
+                cur = nx;
+                css = nss;
+            }
+            {
+                ZDBCRC_STEP(bufn, bufc)
+                if (!more)
+                    break;
+                cur = nx;
+                css = nss;
+            }
+        }
+    } else {
+        for (;;) {
+            ZDBCRC_STEP(bufc, bufn)
+            if (!more)
+                break;
+            cur = nx;
+            css = nss;
 #pragma unroll
-        for (int i = 0; i < K; i++)
-            bufc[i] = bufn[i];
+            for (int i = 0; i < K; i++)
+                bufc[i] = bufn[i];
+        }
     }
+#undef ZDBCRC_STEP
     if (PRIO && lane == 0)
         prog[wid] = 0xFFFFFFFFu; // finished: counts as ahead of everyone
     if (STAMP && lane == 0) {
@@ -862,6 +889,7 @@ const KernelVariant kVariants[] = {
     {"v3_wg768_nt_dyn4c4p32", crc_batch_kernel_v3<768, 6, false, 0, UNIT_OVH, false, true, false, 0, 4, 4, 32>, 768},
     {"v3_wg768_nt_dyn4c4p32_sp_stamp", crc_batch_kernel_v3<768, 6, true, 0, UNIT_OVH, false, true, false, 0, 4, 4, 32, true>, 768},
     {"v3_wg768_nt_dyn4c4p32_sp_noload", crc_batch_kernel_v3<768, 6, false, 0, UNIT_OVH, false, true, true, 0, 4, 4, 32, true>, 768},
+    {"v3_wg768_nt_dyn4c4p32_sp_pp", crc_batch_kernel_v3<768, 6, false, 0, UNIT_OVH, false, true, false, 0, 4, 4, 32, true, true>, 768},
 };
 constexpr int kNumVariants = (int)(sizeof(kVariants) / sizeof(kVariants[0]));
 std::atomic<int> g_variant{-1};
