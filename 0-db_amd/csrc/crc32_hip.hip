@@ -74,6 +74,8 @@ constexpr uint64_t DYN_MIN_UNITS_PER_WAVE = 4096;
 // ... and no record spans more than this many chunks (each chunk cut of a
 // record is one same-address atomic XOR: one huge record would serialise them)
 constexpr uint64_t DYN_MAX_CHUNKS_PER_RECORD = 64;
+// records up to this many bytes take the small-record loop shape (PP)
+constexpr uint64_t SMALL_RECORD_MAX = 4096;
 
 static_assert(ZDBCRC_LDS_DW % 4 == 0, "LDS image must be 16-byte granular");
 static_assert(ZDBCRC_LDS_DW * 4 * WG_PER_CU <= 160 * 1024, "LDS budget");
@@ -542,7 +544,8 @@ __device__ __forceinline__ uint64_t block_excl_scan64(uint64_t v, uint64_t *wsum
 // NTL: payload loads carry the nontemporal hint (read once, never reused)
 // NOLOAD: timing diagnostic only (no payload loads: the compute floor; wrong checksums)
 // PP: the loop is unrolled twice and the two load buffers swap roles instead
-// of being copied (16 v_mov per superstep)
+// of being copied (16 v_mov per superstep); 1 = always, 2 = only when every
+// record of the batch fits one superstep (planner block maxima)
 // DYN > 0: tail pool.  Static slices cover the first (16 - DYN)/16 of the unit
 // space; the rest is split into DYN_POOLS pools (pool = blockIdx mod DYN_POOLS) of
 // CPW chunks per wave, claimed with one atomicAdd each as waves run out of
@@ -551,7 +554,7 @@ __device__ __forceinline__ uint64_t block_excl_scan64(uint64_t v, uint64_t *wsum
 // are flushed with atomic XOR at each claim (at most 2 are pending then).
 template <int WGT, int WPE, bool STAMP = false, int PRIO = 0, uint32_t UO = UNIT_OVH, bool NOZ = false,
           bool NTL = false, bool NOLOAD = false, int XM = 0, int DYN = 0, int CPW = 4, uint32_t DYN_POOLS = 8,
-          bool SP = false, bool PP = false>
+          bool SP = false, int PP = 0>
 __global__ __launch_bounds__(WGT, WPE) void crc_batch_kernel_v3(
     const uint8_t *__restrict__ arena, const uint64_t *__restrict__ offsets,
     const uint32_t *__restrict__ lengths, const PlanArgs plan, uint64_t n,
@@ -577,12 +580,12 @@ __global__ __launch_bounds__(WGT, WPE) void crc_batch_kernel_v3(
             const uint32_t b = threadIdx.x * PER + i;
             v[i] = b < plan.nb ? plan.bsum[b] : 0;
             t += v[i];
-            if (DYN) {
+            if (DYN || PP == 2) {
                 const uint32_t q = b < plan.nb ? plan.bmax[b] : 0u;
                 mx = q > mx ? q : mx;
             }
         }
-        if (DYN) {
+        if (DYN || PP == 2) {
             mx = wave_max(mx);
             if ((threadIdx.x & 63u) == 0)
                 wmax[threadIdx.x >> 6] = mx;
@@ -617,6 +620,13 @@ __global__ __launch_bounds__(WGT, WPE) void crc_batch_kernel_v3(
             mxu = wmax[i] > mxu ? wmax[i] : mxu;
         const uint64_t chunk = total * DYN / 16 / ((uint64_t)CPW * nwaves);
         dyn = mxu <= DYN_MAX_CHUNKS_PER_RECORD * chunk;
+    }
+    bool pp = PP == 1;
+    if (PP == 2 && plan.bmax) { // every record within one superstep (+1 piece of misalignment)
+        uint32_t mxu = 0;
+        for (uint32_t i = 0; i < NW; i++)
+            mxu = wmax[i] > mxu ? wmax[i] : mxu;
+        pp = mxu <= UO + 64u * K + 1u;
     }
     const uint64_t Ts = dyn ? total - total * DYN / 16 : total;
     uint64_t ub = Ts * gw / nwaves;
@@ -783,7 +793,7 @@ __global__ __launch_bounds__(WGT, WPE) void crc_batch_kernel_v3(
         if (lane == 0)                                                                                        \
             *dst = x;
 
-    if (PP) { // ping-pong: the two load buffers swap roles, no register copies
+    if (PP && pp) { // ping-pong: the two load buffers swap roles, no register copies
         for (;;) {
             {
                 ZDBCRC_STEP(bufc, bufn)
@@ -889,12 +899,12 @@ const KernelVariant kVariants[] = {
     {"v3_wg768_nt_dyn4c4p32", crc_batch_kernel_v3<768, 6, false, 0, UNIT_OVH, false, true, false, 0, 4, 4, 32>, 768},
     {"v3_wg768_nt_dyn4c4p32_sp_stamp", crc_batch_kernel_v3<768, 6, true, 0, UNIT_OVH, false, true, false, 0, 4, 4, 32, true>, 768},
     {"v3_wg768_nt_dyn4c4p32_sp_noload", crc_batch_kernel_v3<768, 6, false, 0, UNIT_OVH, false, true, true, 0, 4, 4, 32, true>, 768},
-    {"v3_wg768_nt_dyn4c4p32_sp_pp", crc_batch_kernel_v3<768, 6, false, 0, UNIT_OVH, false, true, false, 0, 4, 4, 32, true, true>, 768},
+    {"v3_wg768_nt_dyn4c4p32_sp_pp", crc_batch_kernel_v3<768, 6, false, 0, UNIT_OVH, false, true, false, 0, 4, 4, 32, true, 1>, 768},
 };
 constexpr int kNumVariants = (int)(sizeof(kVariants) / sizeof(kVariants[0]));
 std::atomic<int> g_variant{-1};
 
-const KernelVariant &variant() {
+const KernelVariant &variant(bool /*small: the A/B harness picks by index*/ = false) {
     int v = g_variant.load();
     if (v < 0) {
         const char *e = std::getenv("ZDBCRC_VARIANT");
@@ -906,13 +916,23 @@ const KernelVariant &variant() {
     return kVariants[v];
 }
 #else
-// the product library ships exactly one checksum kernel: tail pool (4/16 of
-// the units, 32 pools, 4 chunks per wave) with static-phase priority, 768
-// threads, nontemporal payload loads; no environment knob
+// the product library ships the checksum kernel in two loop shapes, no
+// environment knob: tail pool (4/16 of the units, 32 pools, 4 chunks per
+// wave) with static-phase priority, 768 threads, nontemporal payload loads
+// (DESIGN.md §4.1); the small-record shape (PP: the loop unrolled twice, load
+// buffers swapping roles instead of 16 register copies per superstep) for
+// batches whose records are known to be <= 4 KiB -- C2 -3.2 %, C2u -3.5 %,
+// but C3 +2.9 % (profiles/r2/ab_pp.jsonl); both shapes are exact for any
+// input, the choice only changes speed.  (One kernel holding both loops
+// needs more than the 80 VGPRs six waves per SIMD allow: 40 B/lane of
+// scratch.)
 const KernelVariant kDefault = {"v3_wg768_nt_dyn4c4p32_sp",
                                 crc_batch_kernel_v3<768, 6, false, 0, UNIT_OVH, false, true, false, 0, 4, 4, 32, true>,
                                 768};
-const KernelVariant &variant() { return kDefault; }
+const KernelVariant kSmall = {"v3_wg768_nt_dyn4c4p32_sp_pp",
+                              crc_batch_kernel_v3<768, 6, false, 0, UNIT_OVH, false, true, false, 0, 4, 4, 32, true, 1>,
+                              768};
+const KernelVariant &variant(bool small = false) { return small ? kSmall : kDefault; }
 #endif
 
 // unit count per record: ovh (the variant's per-record charge) + number of
@@ -1497,6 +1517,25 @@ int zdb_crc32_batch_device(const uint8_t *d_arena, const uint64_t *d_offsets, co
                          static_cast<hipStream_t>(stream));
 }
 
+int zdb_crc32_batch_device_sized(const uint8_t *d_arena, const uint64_t *d_offsets, const uint32_t *d_lengths,
+                                 uint32_t *d_out, size_t n, uint32_t max_length, void *stream) {
+    if (n == 0)
+        return ZDB_CRC32_OK;
+    if (!d_arena || !d_offsets || !d_lengths || !d_out)
+        return ZDB_CRC32_EINVAL;
+    int dev;
+    int rc = current_device(&dev);
+    if (rc)
+        return rc;
+    std::lock_guard<std::mutex> g(g_dev_mu[dev]);
+    DeviceCtx *c;
+    if ((rc = ensure_device(dev, &c)))
+        return rc;
+    const bool small = max_length > 0 && max_length <= SMALL_RECORD_MAX;
+    return enqueue_batch(dev, *c, variant(small), d_arena, d_offsets, d_lengths, d_out, n,
+                         static_cast<hipStream_t>(stream));
+}
+
 int zdb_crc32_verify_device(const uint8_t *d_arena, const uint64_t *d_offsets, const uint32_t *d_lengths,
                             const uint32_t *d_expected, uint32_t *d_out, uint32_t *d_mismatch,
                             uint32_t *d_mismatch_count, uint32_t max_mismatch, size_t n, void *stream) {
@@ -1572,9 +1611,12 @@ int zdb_crc32_batch(const uint8_t *arena, size_t arena_len, const uint64_t *offs
         return ZDB_CRC32_OK;
     if (!arena || !offsets || !lengths || !out)
         return ZDB_CRC32_EINVAL;
-    for (size_t r = 0; r < n; r++) // overflow-safe: offsets[r] may be near UINT64_MAX
+    uint32_t max_len = 0;
+    for (size_t r = 0; r < n; r++) { // overflow-safe: offsets[r] may be near UINT64_MAX
         if (offsets[r] > arena_len || lengths[r] > arena_len - offsets[r])
             return ZDB_CRC32_EINVAL;
+        max_len = lengths[r] > max_len ? lengths[r] : max_len;
+    }
     int dev;
     int rc = current_device(&dev);
     if (rc)
@@ -1619,7 +1661,8 @@ int zdb_crc32_batch(const uint8_t *arena, size_t arena_len, const uint64_t *offs
     uint32_t *hout = reinterpret_cast<uint32_t *>(h.hplan + n * 12 + (n + 1) * 8);
     std::memcpy(ho, offsets, n * 8);
     std::memcpy(hl, lengths, n * 4);
-    const KernelVariant &kv = variant(); // resolved once: the host prefix and the kernel agree on UO
+    // resolved once: the host prefix and the kernel agree on UO
+    const KernelVariant &kv = variant(max_len <= SMALL_RECORD_MAX);
     const UnitCount uc{h.arena, offsets, lengths, n, kv.unit_ovh};
     uint64_t acc = 0;
     for (size_t r = 0; r < n; r++) {
@@ -1854,9 +1897,12 @@ int zdb_crc32_stream_checksum(zdb_crc32_stream_t *s, const uint64_t *offsets, co
         return ZDB_CRC32_OK;
     if (!offsets || !lengths || !out)
         return ZDB_CRC32_EINVAL;
-    for (size_t r = 0; r < n; r++) // overflow-safe bounds against the appended bytes
+    uint32_t max_len = 0;
+    for (size_t r = 0; r < n; r++) { // overflow-safe bounds against the appended bytes
         if (offsets[r] > s->fill || lengths[r] > s->fill - offsets[r])
             return ZDB_CRC32_EINVAL;
+        max_len = lengths[r] > max_len ? lengths[r] : max_len;
+    }
     if (hipSetDevice(s->dev) != hipSuccess)
         return ZDB_CRC32_ELAUNCH;
     const size_t need = n * 16 + 64;
@@ -1885,7 +1931,8 @@ int zdb_crc32_stream_checksum(zdb_crc32_stream_t *s, const uint64_t *offsets, co
         DeviceCtx *c;
         int rc = ensure_device(s->dev, &c);
         if (!rc)
-            rc = enqueue_batch(s->dev, *c, variant(), s->d_image, reinterpret_cast<const uint64_t *>(s->d_desc),
+            rc = enqueue_batch(s->dev, *c, variant(max_len <= SMALL_RECORD_MAX), s->d_image,
+                               reinterpret_cast<const uint64_t *>(s->d_desc),
                                reinterpret_cast<const uint32_t *>(s->d_desc + n * 8), d_out, n, s->st);
         if (rc)
             return rc;

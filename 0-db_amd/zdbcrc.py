@@ -63,6 +63,7 @@ _strerror = _fn("zdb_crc32_strerror", C.c_char_p, C.c_int)
 _batch_engine = _fn("zdb_crc32_batch_engine", C.c_char_p)
 _gpu_initialized = _fn("zdb_crc32_gpu_initialized", C.c_int)
 _batch_device = _fn("zdb_crc32_batch_device", C.c_int, vp, vp, vp, vp, C.c_size_t, vp)
+_batch_device_sized = _fn("zdb_crc32_batch_device_sized", C.c_int, vp, vp, vp, vp, C.c_size_t, C.c_uint32, vp)
 _verify_device = _fn("zdb_crc32_verify_device", C.c_int, vp, vp, vp, vp, vp, vp, vp, C.c_uint32,
                      C.c_size_t, vp)
 _batch_host = _fn("zdb_crc32_batch", C.c_int, vp, C.c_size_t, vp, vp, vp, C.c_size_t)
@@ -102,13 +103,15 @@ _encode_batch = _fn("zdb_datafile_encode_batch", C.c_size_t, vp, C.c_size_t, C.c
 EXPORTED = [
     "zdb_crc32_engine_value", "zdb_crc32", "zdb_checksum_crc32", "zdb_crc32_shift",
     "zdb_crc32_combine", "zdb_crc32_table_image", "zdb_crc32_strerror", "zdb_crc32_batch_engine",
-    "zdb_crc32_gpu_initialized", "zdb_crc32_batch_device", "zdb_crc32_verify_device",
+    "zdb_crc32_gpu_initialized", "zdb_crc32_batch_device", "zdb_crc32_batch_device_sized",
+    "zdb_crc32_verify_device",
     "zdb_crc32_batch", "zdb_crc32_device_count", "zdb_crc32_use_device", "zdb_crc32_host_alloc",
     "zdb_crc32_host_free", "zdb_crc32_set_timing",
     "zdb_crc32_kernel_stats", "zdb_synth_fill", "zdb_synth_fill_device", "zdb_synth_zipf_lengths",
     "zdb_datafile_walk", "zdb_datafile_encode_entry", "zdb_datafile_encode_header",
     "zdb_datafile_payloads", "zdb_datafile_encode_batch", "zdb_datafile_check_device",
-    "zdb_datafile_walk_device", "zdb_datafile_scan_device",
+    "zdb_datafile_walk_device", "zdb_datafile_scan_device", "zdb_crc32_stream_open", "zdb_crc32_stream_begin",
+    "zdb_crc32_stream_append", "zdb_crc32_stream_checksum", "zdb_crc32_stream_close",
 ]
 
 RECORD_DTYPE = np.dtype([
@@ -201,8 +204,10 @@ def _dev_check(t, dtype, name):
     return t
 
 
-def batch_device(arena, offsets, lengths, out, stream=None):
-    """out[r] = zdb_crc32(arena[offsets[r]:][:lengths[r]]) on the GPU (async)."""
+def batch_device(arena, offsets, lengths, out, stream=None, max_length: int | None = None):
+    """out[r] = zdb_crc32(arena[offsets[r]:][:lengths[r]]) on the GPU (async).
+    max_length: an upper bound of the lengths the caller knows
+    (zdb_crc32_batch_device_sized), None = unknown."""
     import torch
     _dev_check(arena, torch.uint8, "arena")
     _dev_check(offsets, torch.int64, "offsets")
@@ -211,8 +216,12 @@ def batch_device(arena, offsets, lengths, out, stream=None):
     n = offsets.numel()
     if lengths.numel() != n or out.numel() < n:
         raise ValueError("descriptor sizes differ")
-    _check(_batch_device(arena.data_ptr(), offsets.data_ptr(), lengths.data_ptr(), out.data_ptr(), n,
-                         _stream_handle(stream)), "zdb_crc32_batch_device")
+    if max_length is None:
+        _check(_batch_device(arena.data_ptr(), offsets.data_ptr(), lengths.data_ptr(), out.data_ptr(), n,
+                             _stream_handle(stream)), "zdb_crc32_batch_device")
+    else:
+        _check(_batch_device_sized(arena.data_ptr(), offsets.data_ptr(), lengths.data_ptr(), out.data_ptr(), n,
+                                   max_length, _stream_handle(stream)), "zdb_crc32_batch_device_sized")
     return out
 
 

@@ -81,6 +81,15 @@ int zdb_crc32_batch_device(const uint8_t *d_arena, const uint64_t *d_offsets,
                            const uint32_t *d_lengths, uint32_t *d_out,
                            size_t n, void *stream);
 
+/* As zdb_crc32_batch_device, for a caller that knows an upper bound of its
+ * record lengths (max_length, 0 = unknown): batches of records <= 4 KiB
+ * (fixed-size values, pipelined small SETs) take the small-record loop shape
+ * of the kernel.  Exact for any input; a record longer than the bound only
+ * costs speed.  The host-buffer entry points measure the bound themselves. */
+int zdb_crc32_batch_device_sized(const uint8_t *d_arena, const uint64_t *d_offsets,
+                                 const uint32_t *d_lengths, uint32_t *d_out,
+                                 size_t n, uint32_t max_length, void *stream);
+
 /* Device-resident verify: as zdb_crc32_batch_device, then compares with
  * d_expected[r] (the stored `integrity` field, data.h:60).  Mismatching record
  * indices are appended (unordered) to d_mismatch[0..max_mismatch) and

@@ -437,3 +437,36 @@ def test_batched_check_empty_payload_key_past_end(dev, oracle_c, integrity, want
     dev.datafile_check_device(d_img, torch.tensor(offs, dtype=torch.int64, device="cuda"), res)
     torch.cuda.synchronize()
     assert int(res.cpu()[0]) == want
+
+
+@pytest.mark.parametrize("case", ["fixed4k", "fixed4k_misaligned", "small_mixed", "hint_too_small"])
+def test_small_record_shape(dev, oracle_c, case):
+    """zdb_crc32_batch_device_sized: the small-record loop shape (records <=
+    4 KiB known to the caller) is bit-exact -- also when the caller's bound is
+    wrong (a 300 KiB record under a 4 KiB hint only costs speed)"""
+    rng = np.random.default_rng(7)
+    if case.startswith("fixed4k"):
+        n = 3000
+        lens = np.full(n, 4096, np.int64)
+        stride = 4096 if case == "fixed4k" else 4096 + 26
+        offs = np.arange(n, dtype=np.int64) * stride + (0 if case == "fixed4k" else 26)
+    else:
+        lens = rng.integers(0, 4097, 5000).astype(np.int64)
+        if case == "hint_too_small":
+            lens[1234] = 300_000
+        offs = np.zeros(len(lens), np.int64)
+        offs[1:] = np.cumsum(lens[:-1] + rng.integers(0, 5, len(lens) - 1))
+    total = int(offs[-1] + lens[-1])
+    arena = oracle.splitmix_bytes(total, 0x5A11)
+    a = torch.zeros(total + 64, dtype=torch.uint8, device="cuda")
+    a[:total] = torch.from_numpy(arena).cuda()
+    o = torch.from_numpy(offs).cuda()
+    l = torch.from_numpy(lens.astype(np.int32)).cuda()
+    out = torch.full((len(lens),), -1, dtype=torch.int32, device="cuda")
+    want = oracle_c.batch(arena, offs, lens)
+    for _ in range(2):  # both counter parities of the tail pool
+        dev.batch_device(a, o, l, out, max_length=4096)
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(out.cpu().numpy().view(np.uint32), want)
+    # the host-buffer entry picks the shape from the lengths it is given
+    np.testing.assert_array_equal(dev.batch_host(arena, offs.astype(np.uint64), lens.astype(np.uint32)), want)
