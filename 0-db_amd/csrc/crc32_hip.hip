@@ -37,6 +37,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <algorithm>
 #include <atomic>
 #include <map>
 #include <mutex>
@@ -1284,7 +1285,7 @@ int ensure_device(int dev, DeviceCtx **out_ctx) {
 // (host-planned batches); nullptr -> computed on the device by the scan
 int enqueue_batch(int dev, DeviceCtx &c, const KernelVariant &kv, const uint8_t *arena, const uint64_t *offsets,
                   const uint32_t *lengths, uint32_t *out, uint64_t n, hipStream_t st,
-                  const uint64_t *d_unit_start = nullptr) {
+                  const uint64_t *d_unit_start = nullptr, uint32_t grid_wgs = 0) {
     if (n > 0xFFFFFFFFull) // record indices are 32-bit on the device (cut lists, mismatch indices)
         return ZDB_CRC32_EINVAL;
     // planner blocks: 2^lg records each (n + 1 entries), at most PLAN_MAX_BLOCKS
@@ -1333,7 +1334,12 @@ int enqueue_batch(int dev, DeviceCtx &c, const KernelVariant &kv, const uint8_t 
         return ZDB_CRC32_ELAUNCH;
     }
 
-    const uint32_t grid = (uint32_t)(c.cus * kv.wgs_per_cu);
+    // full persistent grid, or fewer workgroups for a host-planned batch
+    // that cannot occupy them (one SET value: the table fill of 512
+    // workgroups would cost more than the checksum)
+    uint32_t grid = (uint32_t)(c.cus * kv.wgs_per_cu);
+    if (grid_wgs && grid_wgs < grid)
+        grid = grid_wgs;
     const uint32_t max_waves = grid * (uint32_t)(kv.threads / 64);
     hipEvent_t e0 = nullptr, e1 = nullptr;
     std::unique_lock<std::mutex> tl(g_mu, std::defer_lock);
@@ -1383,6 +1389,28 @@ struct HostStaging {
     hipStream_t st = nullptr;
 };
 HostStaging g_host_staging[64];
+
+// pinned allocations made by zdb_crc32_host_alloc (base -> bytes, including
+// 64 readable bytes past what the caller asked for): a host-buffer batch
+// whose arena lies inside one is read by the kernel in place, over PCIe
+// (zero-copy), with no staging copy
+std::mutex g_pin_mu;
+std::map<uintptr_t, size_t> g_pinned;
+
+const uint8_t *pinned_device_view(const uint8_t *arena, size_t len) {
+    const uintptr_t a = reinterpret_cast<uintptr_t>(arena);
+    std::lock_guard<std::mutex> g(g_pin_mu);
+    auto it = g_pinned.upper_bound(a);
+    if (it == g_pinned.begin())
+        return nullptr;
+    --it;
+    if (a + len + 16 > it->first + it->second) // the kernel reads up to the next 16-byte boundary
+        return nullptr;
+    void *dp = nullptr;
+    if (hipHostGetDevicePointer(&dp, reinterpret_cast<void *>(it->first), 0) != hipSuccess || !dp)
+        return nullptr;
+    return static_cast<const uint8_t *>(dp) + (a - it->first);
+}
 
 size_t plan_bytes(size_t n) { return n * 8 + n * 4 + (n + 1) * 8 + n * 4 + 64; }
 
@@ -1628,8 +1656,11 @@ int zdb_crc32_batch(const uint8_t *arena, size_t arena_len, const uint64_t *offs
     HostStaging &h = g_host_staging[dev];
     if (!h.st && hipStreamCreateWithFlags(&h.st, hipStreamNonBlocking) != hipSuccess)
         return ZDB_CRC32_ELAUNCH;
+    // an arena in memory from zdb_crc32_host_alloc is read in place (C5:
+    // one SET value costs a launch and a sync instead of two copies more)
+    const uint8_t *d_arena = pinned_device_view(arena, arena_len);
     const size_t abytes = arena_len + 16;
-    if (h.arena_bytes < abytes) {
+    if (!d_arena && h.arena_bytes < abytes) {
         if (h.arena)
             hipFree(h.arena);
         h.arena = nullptr;
@@ -1663,7 +1694,9 @@ int zdb_crc32_batch(const uint8_t *arena, size_t arena_len, const uint64_t *offs
     std::memcpy(hl, lengths, n * 4);
     // resolved once: the host prefix and the kernel agree on UO
     const KernelVariant &kv = variant(max_len <= SMALL_RECORD_MAX);
-    const UnitCount uc{h.arena, offsets, lengths, n, kv.unit_ovh};
+    if (!d_arena)
+        d_arena = h.arena;
+    const UnitCount uc{d_arena, offsets, lengths, n, kv.unit_ovh};
     uint64_t acc = 0;
     for (size_t r = 0; r < n; r++) {
         hu[r] = acc;
@@ -1674,10 +1707,24 @@ int zdb_crc32_batch(const uint8_t *arena, size_t arena_len, const uint64_t *offs
     uint32_t *d_len = reinterpret_cast<uint32_t *>(h.plan + n * 8);
     uint64_t *d_us = reinterpret_cast<uint64_t *>(h.plan + n * 12);
     uint32_t *d_out = reinterpret_cast<uint32_t *>(h.plan + n * 12 + (n + 1) * 8);
-    if (hipMemcpyAsync(h.arena, arena, arena_len, hipMemcpyHostToDevice, h.st) != hipSuccess ||
-        hipMemcpyAsync(h.plan, h.hplan, n * 12 + (n + 1) * 8, hipMemcpyHostToDevice, h.st) != hipSuccess)
+    const bool zero_copy = d_arena != h.arena;
+    if (zero_copy) { // the descriptors too are read in place from the pinned plan
+        void *dp = nullptr;
+        if (hipHostGetDevicePointer(&dp, h.hplan, 0) != hipSuccess || !dp)
+            return ZDB_CRC32_ELAUNCH;
+        uint8_t *dplan = static_cast<uint8_t *>(dp);
+        d_off = reinterpret_cast<uint64_t *>(dplan);
+        d_len = reinterpret_cast<uint32_t *>(dplan + n * 8);
+        d_us = reinterpret_cast<uint64_t *>(dplan + n * 12);
+    } else if (hipMemcpyAsync(h.arena, arena, arena_len, hipMemcpyHostToDevice, h.st) != hipSuccess ||
+               hipMemcpyAsync(h.plan, h.hplan, n * 12 + (n + 1) * 8, hipMemcpyHostToDevice, h.st) != hipSuccess) {
         return ZDB_CRC32_ELAUNCH;
-    rc = enqueue_batch(dev, *c, kv, h.arena, d_off, d_len, d_out, n, h.st, d_us);
+    }
+    // workgroups the batch can keep busy (MIN_UNITS_PER_WAVE units per wave)
+    const uint64_t waves = (acc + MIN_UNITS_PER_WAVE - 1) / MIN_UNITS_PER_WAVE;
+    const uint64_t wpw = (uint64_t)(kv.threads / 64);
+    const uint32_t grid_wgs = (uint32_t)std::min<uint64_t>((waves + wpw - 1) / wpw, 1u << 20);
+    rc = enqueue_batch(dev, *c, kv, d_arena, d_off, d_len, d_out, n, h.st, d_us, grid_wgs);
     if (rc)
         return rc;
     if (hipMemcpyAsync(hout, d_out, n * 4, hipMemcpyDeviceToHost, h.st) != hipSuccess)
@@ -1706,14 +1753,21 @@ int zdb_crc32_use_device(int device) {
 void *zdb_crc32_host_alloc(size_t bytes) {
     g_hip_touched = true;
     void *p = nullptr;
-    if (hipHostMalloc(&p, bytes, hipHostMallocDefault) != hipSuccess)
+    if (hipHostMalloc(&p, bytes + 64, hipHostMallocDefault) != hipSuccess)
         return nullptr;
+    std::lock_guard<std::mutex> g(g_pin_mu);
+    g_pinned[reinterpret_cast<uintptr_t>(p)] = bytes + 64;
     return p;
 }
 
 void zdb_crc32_host_free(void *p) {
-    if (p)
-        hipHostFree(p);
+    if (!p)
+        return;
+    {
+        std::lock_guard<std::mutex> g(g_pin_mu);
+        g_pinned.erase(reinterpret_cast<uintptr_t>(p));
+    }
+    hipHostFree(p);
 }
 
 void zdb_crc32_set_timing(int enable) {

@@ -100,9 +100,11 @@ int zdb_crc32_verify_device(const uint8_t *d_arena, const uint64_t *d_offsets,
                             uint32_t *d_mismatch_count, uint32_t max_mismatch,
                             size_t n, void *stream);
 
-/* Host-buffer batch: copies arena[0..arena_len) and the descriptors to the
- * device, runs, copies out[] back, and synchronises.  Pinned host memory
- * (zdb_crc32_host_alloc) gives full PCIe rate. */
+/* Host-buffer batch: out[r] for host descriptors over a host arena,
+ * synchronous.  An arena inside memory from zdb_crc32_host_alloc is read by
+ * the kernel in place over PCIe (zero-copy: one launch, one small copy back);
+ * any other arena is staged to the device first.  The launch is sized to
+ * the batch (one 256 KiB value does not start the whole persistent grid). */
 int zdb_crc32_batch(const uint8_t *arena, size_t arena_len, const uint64_t *offsets,
                     const uint32_t *lengths, uint32_t *out, size_t n);
 
@@ -143,7 +145,8 @@ int zdb_crc32_device_count(void);
  * calls on different devices run concurrently). */
 int zdb_crc32_use_device(int device);
 
-/* pinned host staging for the host-buffer path */
+/* pinned host memory for the host-buffer path (readable 64 bytes past
+ * `bytes`; batches over it are zero-copy) */
 void *zdb_crc32_host_alloc(size_t bytes);
 void zdb_crc32_host_free(void *p);
 

@@ -470,3 +470,38 @@ def test_small_record_shape(dev, oracle_c, case):
         np.testing.assert_array_equal(out.cpu().numpy().view(np.uint32), want)
     # the host-buffer entry picks the shape from the lengths it is given
     np.testing.assert_array_equal(dev.batch_host(arena, offs.astype(np.uint64), lens.astype(np.uint32)), want)
+
+
+@pytest.mark.parametrize("case", ["one_256KiB", "eight_256KiB", "mixed_small", "at_buffer_end"])
+def test_host_batch_zero_copy(dev, oracle_c, case):
+    """zdb_crc32_batch over an arena in zdb_crc32_host_alloc memory: the
+    kernel reads it in place over PCIe (no staging copy) with a launch sized
+    to the batch -- bit-exact, including a record that ends at the last byte
+    the caller asked for"""
+    rng = np.random.default_rng(11)
+    V = 256 * 1024
+    if case == "one_256KiB":
+        offs, lens = np.array([0]), np.array([V])
+    elif case == "eight_256KiB":
+        offs, lens = np.arange(8) * V + 3, np.full(8, V)
+    elif case == "mixed_small":
+        lens = rng.integers(0, 9000, 700)
+        offs = np.zeros(len(lens), np.int64)
+        offs[1:] = np.cumsum(lens[:-1] + 1)
+    else:
+        lens = np.array([1, 4096, 333, 70_001])
+        offs = np.array([0, 5, 4200, 0])
+    total = int((offs + lens).max())
+    pin = dev.PinnedBuffer(total)
+    try:
+        pin.array[:total] = oracle.splitmix_bytes(total, 0xC5 + len(case))
+        if case == "at_buffer_end":
+            offs = offs.copy()
+            offs[-1] = total - int(lens[-1])  # ends exactly at the end of the allocation
+        arena = pin.array[:total]
+        want = oracle_c.batch(np.ascontiguousarray(arena), np.asarray(offs, np.int64), np.asarray(lens, np.int64))
+        for _ in range(3):
+            got = dev.batch_host(arena, np.asarray(offs, np.uint64), np.asarray(lens, np.uint32))
+            np.testing.assert_array_equal(got, want)
+    finally:
+        pin.free()
