@@ -353,6 +353,35 @@ def e2e_legs(offs, lens, seed) -> dict:
     res["set_path_256KiB"] = set_path
     pin.free()
 
+    # f2: pipelined SETs through the two-phase batch harness (zdb-set-pipeline):
+    # values checksummed in one call per receive buffer, GPU (in place, pinned)
+    # vs the scalar engine; crc_s is phase 1 alone
+    import subprocess
+    sys.path.insert(0, str(ROOT / "tests"))
+    from test_set_pipeline import resp_set
+    vals = zdbcrc.synth_fill(64 * V, 0xF2)
+    pipeline = {}
+    for nset in (8, 64, 240):
+        stream = b"".join(resp_set(b"k%05d" % (i % 64), vals[(i % 64) * V:(i % 64 + 1) * V].tobytes()
+                                   if i < 64 else vals[((i * 7) % 64) * V:((i * 7) % 64 + 1) * V].tobytes())
+                          for i in range(nset))
+        row = {}
+        for eng in ("hip", "cpu"):
+            with tempfile.TemporaryDirectory() as td:
+                best = None
+                for _ in range(3):
+                    p = subprocess.run([str(ROOT / "0-db_amd/bin/zdb-set-pipeline"), f"--engine={eng}", "--stats",
+                                        f"--batch={nset}", f"{td}/d{_}"], input=stream, capture_output=True,
+                                       timeout=120)
+                    assert p.returncode == 0, p.stderr[-500:]
+                    st = json.loads(p.stderr.decode().strip().splitlines()[-1])
+                    best = st if best is None or st["crc_s"] < best["crc_s"] else best
+                row[eng] = {"crc_us_per_set": round(best["crc_s"] / nset * 1e6, 2),
+                            "apply_us_per_set": round(best["apply_s"] / nset * 1e6, 2),
+                            "crc_gibs": round(nset * V / best["crc_s"] / GIB, 2)}
+        pipeline[f"{nset}x256KiB"] = row
+    res["set_pipeline"] = pipeline
+
     # zipf batch from pinned host memory: PCIe-inclusive
     total = int(offs[-1] + lens[-1])
     hp = zdbcrc.PinnedBuffer(total + 16)

@@ -505,3 +505,21 @@ def test_host_batch_zero_copy(dev, oracle_c, case):
             np.testing.assert_array_equal(got, want)
     finally:
         pin.free()
+
+
+@pytest.mark.parametrize("batch,datasize", [(1, 600_000), (64, 600_000), (4096, 256 << 20)])
+def test_set_pipeline_gpu_engine_matches_reference_daemon(tmp_path, batch, datasize):
+    """f2: the two-phase SET batch with the GPU engine (values checksummed in
+    place in the pinned receive buffer) against the reference zdbd: replies
+    and datafiles byte-identical (timestamps aside), rotation included"""
+    from test_set_pipeline import ZDBD, build_stream, run_harness, run_reference_zdbd, without_clock
+    if not ZDBD.exists():
+        pytest.skip("oracle/_ref/zdbd not built")
+    stream, nreq = build_stream(5 + batch)
+    reps, ref_files = run_reference_zdbd(stream, nreq, tmp_path, datasize)
+    out, files, stats = run_harness(stream, tmp_path, datasize, "hip", batch)
+    assert '"engine": "hip"' in stats
+    assert out == b"".join(reps)
+    assert sorted(files) == sorted(ref_files)
+    for name in files:
+        assert without_clock(files[name]) == without_clock(ref_files[name]), name
