@@ -435,6 +435,13 @@ int main(int argc, char **argv) {
     uint32_t *vlen = malloc(sizeof(uint32_t) * run.batch);
     if (!buf || !cmpbuf || !req || !crc || !voff || !vlen)
         die("out of memory");
+    if (run.use_gpu) { /* bring the device up before the first request (code object, tables) */
+        uint64_t o = 0;
+        uint32_t l = 64, c = 0;
+        memset(buf, 0, 64);
+        if (g_gpu.batch(buf, 64, &o, &l, &c, 1) != 0)
+            die("GPU engine failed to start (use --engine=cpu)");
+    }
 
     size_t fill = 0, pos = 0;
     int eof = 0, status = 0;
