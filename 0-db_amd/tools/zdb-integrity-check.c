@@ -784,6 +784,10 @@ int main(int argc, char *argv[]) {
      * bits, integrity-check.c:162-165).  Several files: saturate at 255 so a
      * total that is a multiple of 256 cannot read as a clean store. */
     const int code = s.nfiles > 1 ? (total > 255 ? 255 : (int)total) : (int)(total > 0x7FFFFFFF ? 0x7FFFFFFF : total);
+    free(s.reports);
+    free(s.done);
+    free(wa);
+    free(th);
     if (cfg.engine != ENGINE_CPU) {
         /* the GPU start-up thread may still be inside the HIP runtime (auto
          * engine, nothing needed it): end without running teardown under it */

@@ -271,7 +271,7 @@ def cpu_baseline(offs, lens, seed, seconds: float) -> dict | None:
     host on the same records (host copy of rank 0's batch)."""
     import oracle
     import zdbcrc
-    threads = max(1, min(16, int(os.environ.get("OMP_NUM_THREADS", "16")), os.cpu_count() or 1))
+    threads = cpu_threads()
     total = int(offs[-1] + lens[-1])
     arena = zdbcrc.synth_fill(total + 16, seed)
     o = offs.astype(np.uint64)
@@ -303,7 +303,61 @@ def cpu_baseline(offs, lens, seed, seconds: float) -> dict | None:
             "sample": f"full rank-0 batch ({len(lens)} records, {total} B) x {passes} passes on {threads} "
                       f"threads ({seconds:.0f}+ s wall); single-thread {st:.2f} GiB/s on a "
                       f"{b1 >> 20} MiB prefix",
-            "single_thread_gibs": round(st, 3)}
+            "single_thread_gibs": round(st, 3), "cpu_model": cpu_model(),
+            "affinity_cpus": len(os.sched_getaffinity(0)),
+            "threads_rule": "one thread per CPU of this job's share: min(sched_getaffinity, OMP_NUM_THREADS)"}
+
+
+def cpu_threads() -> int:
+    """the CPUs this job may use: its affinity mask, capped by OMP_NUM_THREADS
+    where the launcher sets it (the GPU box gives a one-GPU job 16 of its
+    256 CPUs and says so there)"""
+    n = len(os.sched_getaffinity(0))
+    omp = os.environ.get("OMP_NUM_THREADS")
+    if omp and omp.isdigit() and int(omp) > 0:
+        n = min(n, int(omp))
+    return max(1, n)
+
+
+def cpu_model() -> str:
+    try:
+        for ln in open("/proc/cpuinfo"):
+            if ln.startswith("model name"):
+                return ln.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline_shapes(seconds: float) -> dict:
+    """the reference CPU path on the other BASELINE shapes (C2: 1 Mi x 4 KiB;
+    C4: a 4 GiB prefix of rank 0's C4 shard -- C3 payload sizes inside
+    datafiles), same thread rule, bounded samples"""
+    import oracle
+    import zdbcrc
+    if not oracle.Reference.available():
+        return {}
+    ref, th, out = oracle.Reference(), cpu_threads(), {}
+    shapes = {}
+    o2, l2, s2, _ = make_dataset("fixed4k", 4 << 30, 0)
+    shapes["C2"] = (o2, l2, s2)
+    lay = c4_layout(0)
+    k = int(np.searchsorted(lay["payload_off"] + lay["lens"], 4 << 30))
+    shapes["C4_prefix"] = (lay["payload_off"][:k], lay["lens"][:k], C4_SEED)
+    for name, (o, l, seed) in shapes.items():
+        total = int(o[-1] + l[-1])
+        arena = zdbcrc.synth_fill(total + 16, seed)
+        ou, lu = o.astype(np.uint64), l.astype(np.uint32)
+        passes, t0 = 0, time.perf_counter()
+        while True:
+            ref.batch(arena, ou, lu, threads=th)
+            passes += 1
+            if time.perf_counter() - t0 >= seconds:
+                break
+        out[name] = {"gibs": round(passes * int(l.sum()) / (time.perf_counter() - t0) / GIB, 3),
+                     "records": len(l), "payload_bytes": int(l.sum()), "passes": passes, "threads": th}
+        del arena
+    return out
 
 
 def e2e_legs(offs, lens, seed) -> dict:
@@ -748,6 +802,8 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         log("timing the CPU baseline")
         cpu = cpu_baseline(offs, lens, seed, args.cpu_seconds)
+        if not args.no_extra:
+            extra["cpu_baseline_shapes"] = cpu_baseline_shapes(args.cpu_seconds / 2)
 
     parities = gather_ranks(parity, world)
     if rank == 0:
