@@ -523,3 +523,18 @@ def test_set_pipeline_gpu_engine_matches_reference_daemon(tmp_path, batch, datas
     assert sorted(files) == sorted(ref_files)
     for name in files:
         assert without_clock(files[name]) == without_clock(ref_files[name]), name
+
+
+@pytest.mark.parametrize("name", ["clean", "damaged", "cut", "stops_at_bad_file"])
+def test_index_verify_gpu_engine(tmp_path, name):
+    """f4: zdb-index-verify with the GPU engine against the reference
+    index-rebuild + index-dump (tests/test_index_verify.py)"""
+    from test_index_verify import NAMESPACES, REF, make_ns, oracle_corrupt, reference_live, tool_live
+    if not (REF / "index-rebuild").exists():
+        pytest.skip("oracle/_ref index tools not built")
+    ns = make_ns(tmp_path, NAMESPACES[name])
+    want = reference_live(tmp_path, ns)
+    live, corrupt, p = tool_live(ns, "hip")
+    assert live == want
+    assert corrupt == oracle_corrupt(ns, live)
+    assert p.returncode == len(corrupt)

@@ -68,3 +68,17 @@ def test_sanitized_set_pipeline(tmp_path, batch):
         assert p.returncode == 0
         outs[tag] = p.stdout
     assert outs["san"] == outs["std"]
+
+
+def test_sanitized_index_verify(tmp_path):
+    from test_index_verify import NAMESPACES, make_ns
+    for name, files in NAMESPACES.items():
+        ns = make_ns(tmp_path / name, files)
+        outs = []
+        for exe in (SAN / "zdb-index-verify", ROOT / "0-db_amd" / "bin" / "zdb-index-verify"):
+            p = subprocess.run([str(exe), "--engine=cpu", "--list", str(ns)], capture_output=True, env=ENV,
+                               timeout=120)
+            err = p.stderr.decode()
+            assert "Sanitizer" not in err and "runtime error" not in err, err[-3000:]
+            outs.append((p.stdout, p.returncode))
+        assert outs[0] == outs[1]
