@@ -481,10 +481,10 @@ __device__ __forceinline__ void load_superstep_v3(const SegCtx &s, uint32_t ss, 
     }
 }
 
-template <bool NOZ = false>
+template <int NOZ = 0>
 __device__ __forceinline__ uint32_t seg_value_v3(const Seg &sg, uint32_t acc, uint32_t lane, const uint32_t *lds,
                                                  const uint32_t *__restrict__ tables) {
-    uint32_t x = wave_xor_scalar(lane_place(acc, lane, lds));
+    uint32_t x = wave_xor_scalar(NOZ >= 2 ? acc : lane_place(acc, lane, lds));
     if (!NOZ && sg.z)
         x = uniform_shift(x, tables + ZDBCRC_OFF_Z + sg.z * SCH * 32);
     // shift over the record pieces after the segment: one round per nonzero
@@ -541,7 +541,8 @@ __device__ __forceinline__ uint64_t block_excl_scan64(uint64_t v, uint64_t *wsum
 // (arrival order at a per-CU counter, keyed by the hardware CU id): issue
 // arbitration favours the older workgroup, so the younger one runs on a
 // priority one step (2) or two steps (3) above it.
-// NOZ: timing diagnostic only (skips the trailing-pad shift: wrong checksums)
+// NOZ: timing diagnostic only (1: skips the trailing-pad shift, 2: also the
+// lane placement -- wrong checksums)
 // NTL: payload loads carry the nontemporal hint (read once, never reused)
 // NOLOAD: timing diagnostic only (no payload loads: the compute floor; wrong checksums)
 // PP: the loop is unrolled twice and the two load buffers swap roles instead
@@ -553,7 +554,7 @@ __device__ __forceinline__ uint64_t block_excl_scan64(uint64_t v, uint64_t *wsum
 // work, so waves that the arbitration favours take more of the tail and the
 // launch does not end on its slowest waves.  Cut partials of finished ranges
 // are flushed with atomic XOR at each claim (at most 2 are pending then).
-template <int WGT, int WPE, bool STAMP = false, int PRIO = 0, uint32_t UO = UNIT_OVH, bool NOZ = false,
+template <int WGT, int WPE, bool STAMP = false, int PRIO = 0, uint32_t UO = UNIT_OVH, int NOZ = 0,
           bool NTL = false, bool NOLOAD = false, int XM = 0, int DYN = 0, int CPW = 4, uint32_t DYN_POOLS = 8,
           bool SP = false, int PP = 0>
 __global__ __launch_bounds__(WGT, WPE) void crc_batch_kernel_v3(
@@ -901,6 +902,8 @@ const KernelVariant kVariants[] = {
     {"v3_wg768_nt_dyn4c4p32_sp_stamp", crc_batch_kernel_v3<768, 6, true, 0, UNIT_OVH, false, true, false, 0, 4, 4, 32, true>, 768},
     {"v3_wg768_nt_dyn4c4p32_sp_noload", crc_batch_kernel_v3<768, 6, false, 0, UNIT_OVH, false, true, true, 0, 4, 4, 32, true>, 768},
     {"v3_wg768_nt_dyn4c4p32_sp_pp", crc_batch_kernel_v3<768, 6, false, 0, UNIT_OVH, false, true, false, 0, 4, 4, 32, true, 1>, 768},
+    {"v3_wg768_nt_dyn4c4p32_sp_noz", crc_batch_kernel_v3<768, 6, false, 0, UNIT_OVH, 1, true, false, 0, 4, 4, 32, true>, 768},
+    {"v3_wg768_nt_dyn4c4p32_sp_noz_noplace", crc_batch_kernel_v3<768, 6, false, 0, UNIT_OVH, 2, true, false, 0, 4, 4, 32, true>, 768},
 };
 constexpr int kNumVariants = (int)(sizeof(kVariants) / sizeof(kVariants[0]));
 std::atomic<int> g_variant{-1};
