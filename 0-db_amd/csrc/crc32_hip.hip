@@ -547,7 +547,9 @@ __device__ __forceinline__ uint64_t block_excl_scan64(uint64_t v, uint64_t *wsum
 // NOLOAD: timing diagnostic only (no payload loads: the compute floor; wrong checksums)
 // PP: the loop is unrolled twice and the two load buffers swap roles instead
 // of being copied (16 v_mov per superstep); 1 = always, 2 = only when every
-// record of the batch fits one superstep (planner block maxima)
+// record of the batch fits one superstep (planner block maxima), 3 = always,
+// waiting for the previous loads before issuing the next (one superstep of
+// loads in flight per wave, as the copying loop has)
 // DYN > 0: tail pool.  Static slices cover the first (16 - DYN)/16 of the unit
 // space; the rest is split into DYN_POOLS pools (pool = blockIdx mod DYN_POOLS) of
 // CPW chunks per wave, claimed with one atomicAdd each as waves run out of
@@ -623,7 +625,7 @@ __global__ __launch_bounds__(WGT, WPE) void crc_batch_kernel_v3(
         const uint64_t chunk = total * DYN / 16 / ((uint64_t)CPW * nwaves);
         dyn = mxu <= DYN_MAX_CHUNKS_PER_RECORD * chunk;
     }
-    bool pp = PP == 1;
+    bool pp = PP == 1 || PP == 3;
     if (PP == 2 && plan.bmax) { // every record within one superstep (+1 piece of misalignment)
         uint32_t mxu = 0;
         for (uint32_t i = 0; i < NW; i++)
@@ -774,6 +776,8 @@ __global__ __launch_bounds__(WGT, WPE) void crc_batch_kernel_v3(
             nx = cur;                                                                                         \
             nss = css;                                                                                        \
         }                                                                                                     \
+        if (PP == 3)                                                                                          \
+            __builtin_amdgcn_s_waitcnt(0x0F70);                                                               \
         load_superstep_v3<NTL, NOLOAD>(nx.c, nss, lane, BUFN);                                                \
         if (css == 0 || css + 1 == cur.S)                                                                     \
             acc = superstep<true, XM>(cur.c, acc, BUFC, css, cur.t0, lane, lds);                              \
@@ -902,6 +906,7 @@ const KernelVariant kVariants[] = {
     {"v3_wg768_nt_dyn4c4p32_sp_stamp", crc_batch_kernel_v3<768, 6, true, 0, UNIT_OVH, false, true, false, 0, 4, 4, 32, true>, 768},
     {"v3_wg768_nt_dyn4c4p32_sp_noload", crc_batch_kernel_v3<768, 6, false, 0, UNIT_OVH, false, true, true, 0, 4, 4, 32, true>, 768},
     {"v3_wg768_nt_dyn4c4p32_sp_pp", crc_batch_kernel_v3<768, 6, false, 0, UNIT_OVH, false, true, false, 0, 4, 4, 32, true, 1>, 768},
+    {"v3_wg768_nt_dyn4c4p32_sp_pp_wait", crc_batch_kernel_v3<768, 6, false, 0, UNIT_OVH, false, true, false, 0, 4, 4, 32, true, 3>, 768},
     {"v3_wg768_nt_dyn4c4p32_sp_noz", crc_batch_kernel_v3<768, 6, false, 0, UNIT_OVH, 1, true, false, 0, 4, 4, 32, true>, 768},
     {"v3_wg768_nt_dyn4c4p32_sp_noz_noplace", crc_batch_kernel_v3<768, 6, false, 0, UNIT_OVH, 2, true, false, 0, 4, 4, 32, true>, 768},
 };
