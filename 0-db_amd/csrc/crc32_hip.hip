@@ -928,18 +928,19 @@ const KernelVariant &variant(bool /*small: the A/B harness picks by index*/ = fa
 // the product library ships the checksum kernel in two loop shapes, no
 // environment knob: tail pool (4/16 of the units, 32 pools, 4 chunks per
 // wave) with static-phase priority, 768 threads, nontemporal payload loads
-// (DESIGN.md §4.1); the small-record shape (PP: the loop unrolled twice, load
-// buffers swapping roles instead of 16 register copies per superstep) for
-// batches whose records are known to be <= 4 KiB -- C2 -3.2 %, C2u -3.5 %,
-// but C3 +2.9 % (profiles/r2/ab_pp.jsonl); both shapes are exact for any
-// input, the choice only changes speed.  (One kernel holding both loops
+// (DESIGN.md §4.1); the small-record shape (PP 3: the loop unrolled twice,
+// load buffers swapping roles instead of 16 register copies per superstep,
+// the next loads issued once the previous ones have landed) for batches
+// whose records are known to be <= 4 KiB -- C2 -3.7 %, C2u -3.9 %, but C3
+// +4 % (profiles/r2/ab_ppw.jsonl); both shapes are exact for any input, the
+// choice only changes speed.  (One kernel holding both loops
 // needs more than the 80 VGPRs six waves per SIMD allow: 40 B/lane of
 // scratch.)
 const KernelVariant kDefault = {"v3_wg768_nt_dyn4c4p32_sp",
                                 crc_batch_kernel_v3<768, 6, false, 0, UNIT_OVH, false, true, false, 0, 4, 4, 32, true>,
                                 768};
-const KernelVariant kSmall = {"v3_wg768_nt_dyn4c4p32_sp_pp",
-                              crc_batch_kernel_v3<768, 6, false, 0, UNIT_OVH, false, true, false, 0, 4, 4, 32, true, 1>,
+const KernelVariant kSmall = {"v3_wg768_nt_dyn4c4p32_sp_pp_wait",
+                              crc_batch_kernel_v3<768, 6, false, 0, UNIT_OVH, false, true, false, 0, 4, 4, 32, true, 3>,
                               768};
 const KernelVariant &variant(bool small = false) { return small ? kSmall : kDefault; }
 #endif
