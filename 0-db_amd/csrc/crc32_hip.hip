@@ -39,6 +39,7 @@
 #include <cstring>
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <map>
 #include <mutex>
 #include <vector>
@@ -1085,6 +1086,22 @@ __global__ void check_finish_kernel(const uint32_t *__restrict__ out, const uint
         result[i] = out[i] == expect[i] ? 1 : 0;
 }
 
+// end of a small host batch (C5 latency path): one wave moves the results
+// into the caller-visible mailbox (mapped, host-coherent memory), re-zeroes
+// the device result buffer for the next batch (so no memset precedes it),
+// and then publishes the batch's sequence number with a system-scope release
+// store.  The host spins on that word: no copy engine, no stream synchronize.
+__global__ __launch_bounds__(64) void publish_kernel(uint32_t *__restrict__ d_out, uint32_t *__restrict__ mbox_out,
+                                                      uint32_t n, uint32_t *mbox_seq, uint32_t seq) {
+    for (uint32_t i = threadIdx.x; i < n; i += 64) {
+        mbox_out[i] = d_out[i];
+        d_out[i] = 0;
+    }
+    __threadfence_system();
+    if (threadIdx.x == 0)
+        __hip_atomic_store(mbox_seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 #ifdef ZDBCRC_DIAG
 // read-only streaming probe (measurement aid): XOR of every 16-byte word,
 // one dword written per workgroup -- the achievable HBM read ceiling the
@@ -1292,9 +1309,10 @@ int ensure_device(int dev, DeviceCtx **out_ctx) {
 // enqueue plan + main kernel; caller holds the device's g_dev_mu
 // d_unit_start: the per-record unit prefix when the caller already has it
 // (host-planned batches); nullptr -> computed on the device by the scan
+// out_zeroed: a host-planned batch whose out[] is already zero (latency path)
 int enqueue_batch(int dev, DeviceCtx &c, const KernelVariant &kv, const uint8_t *arena, const uint64_t *offsets,
                   const uint32_t *lengths, uint32_t *out, uint64_t n, hipStream_t st,
-                  const uint64_t *d_unit_start = nullptr, uint32_t grid_wgs = 0) {
+                  const uint64_t *d_unit_start = nullptr, uint32_t grid_wgs = 0, bool out_zeroed = false) {
     if (n > 0xFFFFFFFFull) // record indices are 32-bit on the device (cut lists, mismatch indices)
         return ZDB_CRC32_EINVAL;
     // planner blocks: 2^lg records each (n + 1 entries), at most PLAN_MAX_BLOCKS
@@ -1339,7 +1357,7 @@ int enqueue_batch(int dev, DeviceCtx &c, const KernelVariant &kv, const uint8_t 
         if (hipGetLastError() != hipSuccess)
             return ZDB_CRC32_ELAUNCH;
         plan = PlanArgs{local, bsum, (uint32_t)nb, lg, bmax};
-    } else if (hipMemsetAsync(out, 0, n * sizeof(uint32_t), st) != hipSuccess) {
+    } else if (!out_zeroed && hipMemsetAsync(out, 0, n * sizeof(uint32_t), st) != hipSuccess) {
         return ZDB_CRC32_ELAUNCH;
     }
 
@@ -1389,14 +1407,47 @@ int enqueue_batch(int dev, DeviceCtx &c, const KernelVariant &kv, const uint8_t 
     return ZDB_CRC32_OK;
 }
 
+// batches of at most this many records end in publish_kernel (C5 latency path)
+constexpr size_t MAILBOX_RECORDS = 4096;
+
 struct HostStaging {
     uint8_t *arena = nullptr; // device copy of the caller's arena
     size_t arena_bytes = 0;
     uint8_t *plan = nullptr;  // device: offsets | lengths | unit_start | out
     uint8_t *hplan = nullptr; // pinned host mirror of plan
     size_t n_cap = 0;
+    bool out_zeroed = false;  // the device out[] of plan is all zero
+    uint32_t *mbox = nullptr; // mapped host-coherent: seq word, pad, MAILBOX_RECORDS results
+    uint32_t *d_mbox = nullptr;
+    uint32_t seq = 0;
     hipStream_t st = nullptr;
 };
+
+constexpr size_t MAILBOX_PAD = 16; // dwords before the results (the seq word's own 64 bytes)
+
+// wait for publish_kernel's sequence word; a failed or faulted stream ends
+// the wait through hipStreamQuery, a long batch through a blocking sync
+int wait_mailbox(HostStaging &h, uint32_t seq) {
+    const auto t0 = std::chrono::steady_clock::now();
+    for (uint32_t spins = 1;; spins++) {
+        if (__atomic_load_n(h.mbox, __ATOMIC_ACQUIRE) == seq)
+            return ZDB_CRC32_OK;
+#if defined(__x86_64__)
+        __builtin_ia32_pause();
+#endif
+        if ((spins & 255) != 0)
+            continue;
+        const hipError_t q = hipStreamQuery(h.st);
+        if (q != hipSuccess && q != hipErrorNotReady)
+            return ZDB_CRC32_ELAUNCH;
+        if (q == hipErrorNotReady && std::chrono::steady_clock::now() - t0 < std::chrono::microseconds(500))
+            continue;
+        if (q == hipErrorNotReady && hipStreamSynchronize(h.st) != hipSuccess)
+            return ZDB_CRC32_ELAUNCH;
+        // the stream has drained: the word is there, or the batch failed
+        return __atomic_load_n(h.mbox, __ATOMIC_ACQUIRE) == seq ? ZDB_CRC32_OK : ZDB_CRC32_ELAUNCH;
+    }
+}
 HostStaging g_host_staging[64];
 
 // pinned allocations made by zdb_crc32_host_alloc (base -> bytes, including
@@ -1686,12 +1737,27 @@ int zdb_crc32_batch(const uint8_t *arena, size_t arena_len, const uint64_t *offs
             hipHostFree(h.hplan);
         h.plan = nullptr;
         h.hplan = nullptr;
+        h.out_zeroed = false;
         if (hipMalloc(&h.plan, plan_bytes(n)) != hipSuccess ||
             hipHostMalloc(&h.hplan, plan_bytes(n), hipHostMallocDefault) != hipSuccess) {
             h.n_cap = 0;
             return ZDB_CRC32_ENOMEM;
         }
         h.n_cap = n;
+    }
+    const bool mailbox = n <= MAILBOX_RECORDS;
+    if (mailbox && !h.mbox) {
+        void *m = nullptr, *dm = nullptr;
+        if (hipHostMalloc(&m, (MAILBOX_PAD + MAILBOX_RECORDS) * 4, hipHostMallocMapped | hipHostMallocCoherent) !=
+            hipSuccess)
+            return ZDB_CRC32_ENOMEM;
+        if (hipHostGetDevicePointer(&dm, m, 0) != hipSuccess || !dm) {
+            hipHostFree(m);
+            return ZDB_CRC32_ELAUNCH;
+        }
+        std::memset(m, 0, (MAILBOX_PAD + MAILBOX_RECORDS) * 4);
+        h.mbox = static_cast<uint32_t *>(m);
+        h.d_mbox = static_cast<uint32_t *>(dm);
     }
     // host-side planning: the descriptors and the unit prefix go over in one
     // copy, so a small batch (one SET value) needs no device scan
@@ -1733,9 +1799,23 @@ int zdb_crc32_batch(const uint8_t *arena, size_t arena_len, const uint64_t *offs
     const uint64_t waves = (acc + MIN_UNITS_PER_WAVE - 1) / MIN_UNITS_PER_WAVE;
     const uint64_t wpw = (uint64_t)(kv.threads / 64);
     const uint32_t grid_wgs = (uint32_t)std::min<uint64_t>((waves + wpw - 1) / wpw, 1u << 20);
-    rc = enqueue_batch(dev, *c, kv, d_arena, d_off, d_len, d_out, n, h.st, d_us, grid_wgs);
+    const bool zeroed = h.out_zeroed;
+    h.out_zeroed = false; // until publish_kernel has run to the end
+    rc = enqueue_batch(dev, *c, kv, d_arena, d_off, d_len, d_out, n, h.st, d_us, grid_wgs, zeroed && mailbox);
     if (rc)
         return rc;
+    if (mailbox) { // C5 latency path: results through the mailbox
+        const uint32_t seq = ++h.seq ? h.seq : ++h.seq; // never 0, the mailbox's initial value
+        hipLaunchKernelGGL(publish_kernel, dim3(1), dim3(64), 0, h.st, d_out, h.d_mbox + MAILBOX_PAD, (uint32_t)n,
+                           h.d_mbox, seq);
+        if (hipGetLastError() != hipSuccess)
+            return ZDB_CRC32_ELAUNCH;
+        if ((rc = wait_mailbox(h, seq)))
+            return rc;
+        h.out_zeroed = true;
+        std::memcpy(out, h.mbox + MAILBOX_PAD, n * 4);
+        return ZDB_CRC32_OK;
+    }
     if (hipMemcpyAsync(hout, d_out, n * 4, hipMemcpyDeviceToHost, h.st) != hipSuccess)
         return ZDB_CRC32_ELAUNCH;
     if (hipStreamSynchronize(h.st) != hipSuccess)

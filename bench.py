@@ -363,7 +363,8 @@ def cpu_baseline_shapes(seconds: float) -> dict:
 def e2e_legs(offs, lens, seed) -> dict:
     """Host-memory paths, reported beside the
     device-resident number: the SET path's 256 KiB value through the
-    host-buffer entry (pinned staging, H2D + kernel + D2H), the zipf batch
+    host-buffer entry (zero-copy from pinned memory, results through the
+    mailbox), the zipf batch
     from pinned host memory (PCIe-inclusive rate), and the integrity-check
     tool on a 256 MiB datafile (65,000 x 4 KiB, as SURVEY §6) against the
     reference tool and the scalar engine."""

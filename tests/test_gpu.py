@@ -525,6 +525,25 @@ def test_set_pipeline_gpu_engine_matches_reference_daemon(tmp_path, batch, datas
         assert without_clock(files[name]) == without_clock(ref_files[name]), name
 
 
+def test_set_pipeline_auto_engine_splits_batches(tmp_path):
+    """--engine=auto: batches of at least 512 KiB of values on the GPU, the
+    smaller ones on the scalar engine, replies and datafiles still those of
+    the reference zdbd"""
+    import json
+    from test_set_pipeline import ZDBD, build_stream, run_harness, run_reference_zdbd, without_clock
+    if not ZDBD.exists():
+        pytest.skip("oracle/_ref/zdbd not built")
+    stream, nreq = build_stream(31)  # 4 of its 17 batches of 24 reach 512 KiB
+    reps, ref_files = run_reference_zdbd(stream, nreq, tmp_path, 600_000)
+    out, files, stats = run_harness(stream, tmp_path, 600_000, "auto", 24, from_file=True)
+    st = json.loads(stats.strip().splitlines()[-1])
+    assert st["engine"] == "auto" and 0 < st["gpu_batches"] < st["batches"]
+    assert out == b"".join(reps)
+    assert sorted(files) == sorted(ref_files)
+    for name in files:
+        assert without_clock(files[name]) == without_clock(ref_files[name]), name
+
+
 @pytest.mark.parametrize("name", ["clean", "damaged", "cut", "stops_at_bad_file"])
 def test_index_verify_gpu_engine(tmp_path, name):
     """f4: zdb-index-verify with the GPU engine against the reference

@@ -10,6 +10,7 @@ integrity-check.  CPU engine here; tests/test_gpu.py repeats it with the GPU
 engine."""
 from __future__ import annotations
 
+import json
 import os
 import signal
 import socket
@@ -115,10 +116,20 @@ def run_reference_zdbd(stream: bytes, nreq: int, tmp: Path, datasize: int):
     return reps, files
 
 
-def run_harness(stream: bytes, tmp: Path, datasize: int, engine: str = "cpu", batch: int = 64):
+def run_harness(stream: bytes, tmp: Path, datasize: int, engine: str = "cpu", batch: int = 64,
+                from_file: bool = False):
+    """from_file: the stream is stdin as a regular file, so one read takes all
+    of it and batches are bounded by --batch alone (a pipe hands over 64 KiB
+    at a time)"""
     out = tmp / f"harness_{engine}_{batch}"
-    p = subprocess.run([str(HARNESS), f"--engine={engine}", f"--datasize={datasize}", f"--batch={batch}", "--stats",
-                        str(out)], input=stream, capture_output=True, timeout=120)
+    args = [str(HARNESS), f"--engine={engine}", f"--datasize={datasize}", f"--batch={batch}", "--stats", str(out)]
+    if from_file:
+        src = tmp / f"stream_{engine}_{batch}"
+        src.write_bytes(stream)
+        with open(src, "rb") as f:
+            p = subprocess.run(args, stdin=f, capture_output=True, timeout=120)
+    else:
+        p = subprocess.run(args, input=stream, capture_output=True, timeout=120)
     assert p.returncode == 0, p.stderr.decode()[-2000:]
     files = {q.name: q.read_bytes() for q in sorted(out.glob("d*"))}
     return p.stdout, files, p.stderr.decode()
@@ -171,3 +182,20 @@ def test_set_pipeline_rejects_other_commands(tmp_path):
     p = subprocess.run([str(HARNESS), "--engine=cpu", str(tmp_path / "d")], input=stream, capture_output=True,
                        timeout=60)
     assert p.returncode == 2 and p.stdout == b"$1\r\na\r\n"
+
+
+@needs_ref
+def test_set_pipeline_auto_engine_without_gpu(tmp_path):
+    """--engine=auto with no usable GPU (this container): the scalar engine
+    alone, same replies and datafiles as the reference daemon"""
+    stream, nreq = build_stream(17)
+    reps, ref_files = run_reference_zdbd(stream, nreq, tmp_path, 600_000)
+    out, files, stats = run_harness(stream, tmp_path, 600_000, "auto", 64, from_file=True)
+    assert out == b"".join(reps)
+    assert sorted(files) == sorted(ref_files)
+    for name in files:
+        assert without_clock(files[name]) == without_clock(ref_files[name]), name
+    st = json.loads(stats.strip().splitlines()[-1])
+    assert st["engine"] in ("cpu", "auto")  # "cpu": no usable GPU, the scalar engine alone
+    if st["engine"] == "cpu":
+        assert st["gpu_batches"] == 0
