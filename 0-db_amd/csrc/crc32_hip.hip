@@ -69,6 +69,11 @@ constexpr uint64_t MIN_UNITS_PER_WAVE = 256;
 // (DYN: 2 launch parities x up to 64 pools, one 128-byte line each)
 constexpr uint32_t SCRATCH_CU_CTR = 131072;
 constexpr uint32_t SCRATCH_DYN_CTR = 132096;
+// C5 latency path: small host batches leave their results in a mapped
+// host-coherent mailbox: [0] the batch's sequence number, [MAILBOX_PAD ..)
+// at most MAILBOX_RECORDS results (publish_kernel)
+constexpr uint32_t MAILBOX_PAD = 16;
+constexpr uint32_t MAILBOX_RECORDS = 1024;
 constexpr uint32_t DYN_MAX_POOLS = 64;
 // the tail pool is used only when every slice holds at least this many units
 // (so every wave reaches the pool, and every pool has waves to drain it)
@@ -913,6 +918,7 @@ const KernelVariant kVariants[] = {
 };
 constexpr int kNumVariants = (int)(sizeof(kVariants) / sizeof(kVariants[0]));
 std::atomic<int> g_variant{-1};
+std::atomic<int> g_host_mode{0};
 
 const KernelVariant &variant(bool /*small: the A/B harness picks by index*/ = false) {
     int v = g_variant.load();
@@ -1087,10 +1093,14 @@ __global__ void check_finish_kernel(const uint32_t *__restrict__ out, const uint
 }
 
 // end of a small host batch (C5 latency path): one wave moves the results
-// into the caller-visible mailbox (mapped, host-coherent memory), re-zeroes
-// the device result buffer for the next batch (so no memset precedes it),
-// and then publishes the batch's sequence number with a system-scope release
-// store.  The host spins on that word: no copy engine, no stream synchronize.
+// into the mailbox (mapped, host-coherent memory), re-zeroes the device
+// result buffer for the next batch (so no memset precedes it), and then
+// publishes the batch's sequence number with a system-scope release store.
+// The host spins on that word: no copy engine, no stream synchronize.  (The
+// same work as an epilogue of the checksum kernel -- the last wave to arrive
+// on a counter publishes -- measured slower: 17.2 vs 16.0 us for one 64 B
+// value, 308 vs 196 us for 8 x 1 MiB, the arrivals being same-address
+// atomics; profiles/r2/c5_host_modes.jsonl.)
 __global__ __launch_bounds__(64) void publish_kernel(uint32_t *__restrict__ d_out, uint32_t *__restrict__ mbox_out,
                                                       uint32_t n, uint32_t *mbox_seq, uint32_t seq) {
     for (uint32_t i = threadIdx.x; i < n; i += 64) {
@@ -1407,23 +1417,19 @@ int enqueue_batch(int dev, DeviceCtx &c, const KernelVariant &kv, const uint8_t 
     return ZDB_CRC32_OK;
 }
 
-// batches of at most this many records end in publish_kernel (C5 latency path)
-constexpr size_t MAILBOX_RECORDS = 4096;
-
 struct HostStaging {
     uint8_t *arena = nullptr; // device copy of the caller's arena
     size_t arena_bytes = 0;
     uint8_t *plan = nullptr;  // device: offsets | lengths | unit_start | out
     uint8_t *hplan = nullptr; // pinned host mirror of plan
     size_t n_cap = 0;
-    bool out_zeroed = false;  // the device out[] of plan is all zero
     uint32_t *mbox = nullptr; // mapped host-coherent: seq word, pad, MAILBOX_RECORDS results
     uint32_t *d_mbox = nullptr;
+    uint32_t *d_mout = nullptr; // device results of the latency path, MAILBOX_RECORDS
+    bool mout_zeroed = false;   // all of d_mout is zero (publish_kernel re-zeroes what a batch used)
     uint32_t seq = 0;
     hipStream_t st = nullptr;
 };
-
-constexpr size_t MAILBOX_PAD = 16; // dwords before the results (the seq word's own 64 bytes)
 
 // wait for publish_kernel's sequence word; a failed or faulted stream ends
 // the wait through hipStreamQuery, a long batch through a blocking sync
@@ -1585,6 +1591,15 @@ const char *zdbcrc_debug_set_variant(int idx) {
     return kVariants[idx].name;
 }
 
+// measurement hook: how a small host batch returns its results (0 the
+// mailbox, as shipped; 1 device memset + copy + stream sync)
+int zdbcrc_debug_set_host_mode(int mode) {
+    if (mode < 0 || mode > 1)
+        return -1;
+    g_host_mode = mode;
+    return 0;
+}
+
 #endif // ZDBCRC_DIAG
 
 int zdb_crc32_batch_device(const uint8_t *d_arena, const uint64_t *d_offsets, const uint32_t *d_lengths,
@@ -1737,7 +1752,6 @@ int zdb_crc32_batch(const uint8_t *arena, size_t arena_len, const uint64_t *offs
             hipHostFree(h.hplan);
         h.plan = nullptr;
         h.hplan = nullptr;
-        h.out_zeroed = false;
         if (hipMalloc(&h.plan, plan_bytes(n)) != hipSuccess ||
             hipHostMalloc(&h.hplan, plan_bytes(n), hipHostMallocDefault) != hipSuccess) {
             h.n_cap = 0;
@@ -1745,9 +1759,12 @@ int zdb_crc32_batch(const uint8_t *arena, size_t arena_len, const uint64_t *offs
         }
         h.n_cap = n;
     }
-    const bool mailbox = n <= MAILBOX_RECORDS;
-    if (mailbox && !h.mbox) {
+    if (n <= MAILBOX_RECORDS && !h.mbox) {
         void *m = nullptr, *dm = nullptr;
+        if (!h.d_mout && hipMalloc(&h.d_mout, MAILBOX_RECORDS * 4) != hipSuccess) {
+            h.d_mout = nullptr;
+            return ZDB_CRC32_ENOMEM;
+        }
         if (hipHostMalloc(&m, (MAILBOX_PAD + MAILBOX_RECORDS) * 4, hipHostMallocMapped | hipHostMallocCoherent) !=
             hipSuccess)
             return ZDB_CRC32_ENOMEM;
@@ -1768,6 +1785,11 @@ int zdb_crc32_batch(const uint8_t *arena, size_t arena_len, const uint64_t *offs
     std::memcpy(ho, offsets, n * 8);
     std::memcpy(hl, lengths, n * 4);
     // resolved once: the host prefix and the kernel agree on UO
+#ifdef ZDBCRC_DIAG
+    const bool mailbox = n <= MAILBOX_RECORDS && g_host_mode.load() == 0; // A/B: 1 = copy + sync
+#else
+    const bool mailbox = n <= MAILBOX_RECORDS;
+#endif
     const KernelVariant &kv = variant(max_len <= SMALL_RECORD_MAX);
     if (!d_arena)
         d_arena = h.arena;
@@ -1799,20 +1821,24 @@ int zdb_crc32_batch(const uint8_t *arena, size_t arena_len, const uint64_t *offs
     const uint64_t waves = (acc + MIN_UNITS_PER_WAVE - 1) / MIN_UNITS_PER_WAVE;
     const uint64_t wpw = (uint64_t)(kv.threads / 64);
     const uint32_t grid_wgs = (uint32_t)std::min<uint64_t>((waves + wpw - 1) / wpw, 1u << 20);
-    const bool zeroed = h.out_zeroed;
-    h.out_zeroed = false; // until publish_kernel has run to the end
-    rc = enqueue_batch(dev, *c, kv, d_arena, d_off, d_len, d_out, n, h.st, d_us, grid_wgs, zeroed && mailbox);
+    if (mailbox) {
+        if (!h.mout_zeroed && hipMemsetAsync(h.d_mout, 0, MAILBOX_RECORDS * 4, h.st) != hipSuccess)
+            return ZDB_CRC32_ELAUNCH;
+        d_out = h.d_mout;
+        h.mout_zeroed = false; // until the batch has published
+    }
+    const uint32_t seq = mailbox ? (++h.seq ? h.seq : ++h.seq) : 0; // never 0, the mailbox's initial value
+    rc = enqueue_batch(dev, *c, kv, d_arena, d_off, d_len, d_out, n, h.st, d_us, grid_wgs, mailbox);
     if (rc)
         return rc;
     if (mailbox) { // C5 latency path: results through the mailbox
-        const uint32_t seq = ++h.seq ? h.seq : ++h.seq; // never 0, the mailbox's initial value
         hipLaunchKernelGGL(publish_kernel, dim3(1), dim3(64), 0, h.st, d_out, h.d_mbox + MAILBOX_PAD, (uint32_t)n,
                            h.d_mbox, seq);
         if (hipGetLastError() != hipSuccess)
             return ZDB_CRC32_ELAUNCH;
         if ((rc = wait_mailbox(h, seq)))
             return rc;
-        h.out_zeroed = true;
+        h.mout_zeroed = true;
         std::memcpy(out, h.mbox + MAILBOX_PAD, n * 4);
         return ZDB_CRC32_OK;
     }

@@ -424,17 +424,22 @@ def e2e_legs(offs, lens, seed) -> dict:
                 for i in range(6 * nset)]
         stream = b"".join(reqs)
         row = {}
-        for eng in ("hip", "cpu"):
+        for eng in ("hip", "auto", "cpu"):
             with tempfile.TemporaryDirectory() as td:
-                p = subprocess.run([str(ROOT / "0-db_amd/bin/zdb-set-pipeline"), f"--engine={eng}", "--stats",
-                                    f"--batch={nset}", f"{td}/d"], input=stream, capture_output=True, timeout=300)
+                # stdin is a file: one read fills the receive buffer, so a batch
+                # is --batch SETs (a pipe would hand over 64 KiB per read)
+                with open(f"{td}/stream", "wb") as f:
+                    f.write(stream)
+                with open(f"{td}/stream", "rb") as f:
+                    p = subprocess.run([str(ROOT / "0-db_amd/bin/zdb-set-pipeline"), f"--engine={eng}", "--stats",
+                                        f"--batch={nset}", f"{td}/d"], stdin=f, capture_output=True, timeout=300)
                 assert p.returncode == 0, p.stderr[-500:]
                 st = json.loads(p.stderr.decode().strip().splitlines()[-1])
             w = max(st["sets_after_first_batch"], 1)
             row[eng] = {"crc_us_per_set": round(st["crc_s_after_first_batch"] / w * 1e6, 2),
                         "apply_us_per_set": round(st["apply_s"] / st["sets"] * 1e6, 2),
                         "crc_gibs": round(w * V / max(st["crc_s_after_first_batch"], 1e-9) / GIB, 2),
-                        "batches": st["batches"], "unchanged": st["unchanged"]}
+                        "batches": st["batches"], "gpu_batches": st["gpu_batches"], "unchanged": st["unchanged"]}
         pipeline[f"{nset}x256KiB"] = row
     res["set_pipeline"] = pipeline
 
