@@ -43,6 +43,7 @@
 // remainder of the record straddling each chunk start).
 
 #include <cstdint>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <mutex>
@@ -64,14 +65,20 @@ constexpr int32_t ST_CONTINUE = -1;
 // follow longer chains
 constexpr uint32_t DEFAULT_LG_CHUNK = 23;
 constexpr uint32_t WALK_T = 256;
-constexpr int SU = 8; // search: KiB per wave iteration
+constexpr int SEARCH_T = 256, SEARCH_SU = 8; // search: threads per chunk, KiB per wave block
+// chains per wave (A2, C2): the lanes of a wave hop in lockstep, each hop
+// waiting for the slowest of its lanes' header loads, so fewer chains per
+// wave on more CUs shorten every hop
+constexpr uint32_t CHAINS_PER_WAVE = 16;
 
 // little-endian u32 at any byte address: two aligned dword loads + one
 // v_alignbyte (reads up to 7 bytes past p; images are readable 16 bytes past
 // their end, as for the checksum kernel)
+typedef const __attribute__((address_space(1))) uint32_t gu32; // global loads, not flat (vmcnt only)
+
 __device__ __forceinline__ uint32_t ld_le32(const uint8_t *p) {
     const uintptr_t a = reinterpret_cast<uintptr_t>(p);
-    const uint32_t *q = reinterpret_cast<const uint32_t *>(a & ~uintptr_t(3));
+    gu32 *q = reinterpret_cast<gu32 *>(a & ~uintptr_t(3));
     return __builtin_amdgcn_alignbyte(q[1], q[0], (uint32_t)(a & 3));
 }
 
@@ -85,7 +92,7 @@ struct Hdr {
 __device__ __forceinline__ Hdr load_hdr(const uint8_t *f, uint64_t len, uint64_t pos) {
     if (pos + 4 <= len) {
         const uintptr_t a = reinterpret_cast<uintptr_t>(f + pos);
-        const uint32_t *q = reinterpret_cast<const uint32_t *>(a & ~uintptr_t(3));
+        gu32 *q = reinterpret_cast<gu32 *>(a & ~uintptr_t(3));
         const uint32_t sh = (uint32_t)(a & 3);
         const uint32_t q0 = q[0], q1 = q[1], q2 = q[2], q3 = q[3], q4 = q[4];
         const uint32_t w0 = __builtin_amdgcn_alignbyte(q1, q0, sh), w1 = __builtin_amdgcn_alignbyte(q2, q1, sh);
@@ -95,22 +102,29 @@ __device__ __forceinline__ Hdr load_hdr(const uint8_t *f, uint64_t len, uint64_t
     return Hdr{f[pos], 0u, 0u}; // no whole header fits: the walk stops on SHORT_HEADER
 }
 
-// one record of the serial walk at pos (datafile.c zdb_datafile_walk):
-// SHORT_HEADER -> not a record; SHORT_PAYLOAD -> a record that ends the walk
-__device__ __forceinline__ int32_t hop(const uint8_t *f, uint64_t len, uint64_t pos, uint64_t &next,
-                                       uint32_t &L, Hdr &h) {
-    h = load_hdr(f, len, pos);
-    const uint64_t hlen = ZDB_ENTRY_HEADER_SIZE + (uint64_t)h.idl;
-    if (pos + hlen > len)
-        return ZDB_WALK_SHORT_HEADER;
-    L = h.L;
-    next = pos + hlen;
-    if (L) {
-        if (next + L > len)
-            return ZDB_WALK_SHORT_PAYLOAD;
-        next += L;
-    }
-    return ST_CONTINUE;
+// the same in two halves, so that a chain can issue the next header's loads
+// and decode them only after this record's stores have been issued
+// (branch-free: a load under a branch makes the compiler wait for it where
+// the branches join).  Within 4 bytes of the file's end no whole header
+// fits: the window then starts 4 bytes earlier, so that it stays within the
+// 16 readable bytes past the end, and only idlength is decoded (the walk
+// stops on SHORT_HEADER); pos >= 28 always (the walk starts at or after the
+// 28-byte datafile header)
+struct RawHdr {
+    uint32_t q0, q1, q2, q3, q4, sh; // sh > 3: window shifted back 4 bytes
+};
+__device__ __forceinline__ RawHdr load_raw(const uint8_t *f, uint64_t len, uint64_t pos) {
+    const uint32_t back = pos + 4 <= len ? 0u : 4u;
+    const uintptr_t a = reinterpret_cast<uintptr_t>(f + pos);
+    gu32 *q = reinterpret_cast<gu32 *>((a & ~uintptr_t(3)) - back);
+    return RawHdr{q[0], q[1], q[2], q[3], q[4], (uint32_t)(a & 3) + back};
+}
+__device__ __forceinline__ Hdr decode(const RawHdr &r) {
+    if (r.sh > 3)
+        return Hdr{__builtin_amdgcn_alignbyte(r.q2, r.q1, r.sh - 4) & 0xFFu, 0u, 0u};
+    const uint32_t w0 = __builtin_amdgcn_alignbyte(r.q1, r.q0, r.sh), w1 = __builtin_amdgcn_alignbyte(r.q2, r.q1, r.sh);
+    const uint32_t w2 = __builtin_amdgcn_alignbyte(r.q3, r.q2, r.sh), w3 = __builtin_amdgcn_alignbyte(r.q4, r.q3, r.sh);
+    return Hdr{w0 & 0xFFu, (w0 >> 8) | (w1 << 24), (w2 >> 8) | (w3 << 24)};
 }
 
 // what a walked record turns into: image offsets of header and payload, and
@@ -128,6 +142,9 @@ enum WalkMode { COUNT = 0, SPEC = 1, EMIT = 2 };
 
 // follow the chain from pos while pos < cend.  SPEC keeps the first kcap
 // records in the chunk's slots; EMIT writes the final descriptors at idx..
+// The next header's loads are issued before this record's stores: the
+// memory counter completes in order, so a store issued first would add its
+// own round trip to every hop of the chain (2.4 -> ~1.2 us per hop).
 template <int MODE>
 __device__ __forceinline__ void walk_chain(const uint8_t *f, uint64_t len, uint64_t pos, uint64_t cend,
                                            uint32_t &count, uint64_t &exit, int32_t &st, RecSlot *slots,
@@ -136,22 +153,36 @@ __device__ __forceinline__ void walk_chain(const uint8_t *f, uint64_t len, uint6
                                            uint32_t *__restrict__ plen, uint32_t *__restrict__ expect) {
     count = 0;
     st = ST_CONTINUE;
+    RawHdr raw{0u, 0u, 0u, 0u, 0u, 4u};
+    if (pos < cend && pos < len)
+        raw = load_raw(f, len, pos);
     while (pos < cend) {
         if (pos >= len) { // clean end of file (pos == len)
             st = ZDB_WALK_OK;
             break;
         }
-        uint64_t next = 0;
-        uint32_t L = 0;
-        Hdr h;
-        const int32_t s = hop(f, len, pos, next, L, h);
-        if (s == ZDB_WALK_SHORT_HEADER) {
-            st = s;
+        // the header at pos (hop of datafile.c zdb_datafile_walk)
+        const Hdr h = decode(raw);
+        const uint32_t hlen = ZDB_ENTRY_HEADER_SIZE + h.idl;
+        if (pos + hlen > len) {
+            st = ZDB_WALK_SHORT_HEADER;
             break;
         }
+        const uint32_t L = h.L;
+        uint64_t next = pos + hlen;
+        int32_t s = ST_CONTINUE;
+        if (L) {
+            if (next + L > len)
+                s = ZDB_WALK_SHORT_PAYLOAD;
+            else
+                next += L;
+        }
+        // the next header (decoded at the top of the next hop, after the stores
+        // below); unconditional -- at the end of the walk it reloads pos
+        raw = load_raw(f, len, s == ST_CONTINUE && next < len ? next : pos);
+        __asm__ volatile("" ::: "memory"); // keep the loads above ahead of the stores below
         if (MODE != COUNT) {
             const bool full = s == ST_CONTINUE && L > 0; // payload present and non-empty
-            const uint32_t hlen = ZDB_ENTRY_HEADER_SIZE + h.idl;
             const uint32_t ex = full ? h.integ : 0u;
             if (MODE == SPEC && count < kcap) {
                 slots[count] = RecSlot{(uint32_t)pos, full ? L : 0u, ex, hlen};
@@ -210,14 +241,91 @@ __device__ __forceinline__ void candidates(const uint32_t (&d)[8], uint32_t (&z)
     }
 }
 
-// A1: speculative start of every chunk (one workgroup of NWS waves per chunk:
-// the waves take interleaved SU-KiB blocks, so a chunk that starts inside a
-// 1 MiB payload is searched NWS blocks at a time)
-__global__ __launch_bounds__(WALK_T) void walk_search_kernel(FileTab t, uint64_t *__restrict__ s_start,
-                                                             int32_t *__restrict__ s_status) {
-    constexpr uint32_t NWS = WALK_T / 64;
+// verified candidates of the SB-byte block at b (16-byte aligned) among the
+// positions [lo, hi): FWD -> the lowest (NONE if none), else the highest (0
+// if none).  Wave-uniform result.  Loads read [p0, p0 + 32) for every lane
+// whose 16 positions meet [lo, hi) (p0 >= 16 whenever lo >= 28, and at most 32
+// bytes past hi: within the file, or within the 16 readable bytes past it)
+template <bool FWD, int SU>
+__device__ __forceinline__ uint64_t scan_block(const uint8_t *f, uint64_t len, uint64_t b, uint64_t lo, uint64_t hi,
+                                               uint32_t lane) {
+    uint4 a0[SU], a1[SU];
+#pragma unroll
+    for (int u = 0; u < SU; u++) { // every load of the block in flight
+        const uint64_t p0 = b + 1024u * u + 16u * lane;
+        if (p0 + 16 > lo && p0 < hi) {
+            a0[u] = *reinterpret_cast<const uint4 *>(f + p0);
+            a1[u] = *reinterpret_cast<const uint4 *>(f + p0 + 16);
+        } else {
+            a0[u] = a1[u] = make_uint4(~0u, ~0u, ~0u, ~0u); // no candidate
+        }
+    }
+    uint64_t found = FWD ? NONE : 0;
+#pragma unroll
+    for (int u = 0; u < SU; u++) {
+        const uint64_t p0 = b + 1024u * u + 16u * lane;
+        const uint32_t d[8] = {a0[u].x, a0[u].y, a0[u].z, a0[u].w, a1[u].x, a1[u].y, a1[u].z, a1[u].w};
+        uint32_t z[4];
+        candidates(d, z);
+        if (z[0] | z[1] | z[2] | z[3]) { // rare: confirm through the successor's back-pointer
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                uint32_t m = z[j];
+                while (m && (!FWD || found == NONE)) {
+                    const uint32_t r = (uint32_t)__builtin_ctz(m) >> 3;
+                    m &= ~(0xFFu << (8 * r));
+                    const uint64_t p = p0 + 4u * j + r;
+                    // the entry's own `previous` (bytes p+5..p+8, still in
+                    // registers) must lie before it: every entry but a file's
+                    // first (offset 28, never a candidate here) points back at
+                    // the entry written just before it (data.c:601).  ~2^-5 of
+                    // the filter's false hits pass, so the header loads below
+                    // stay rare
+                    const uint32_t prev = r == 3 ? d[j + 2] : __builtin_amdgcn_alignbyte(d[j + 2], d[j + 1], r + 1);
+                    if (p >= lo && p < hi && (uint64_t)prev < p) {
+                        const Hdr h = load_hdr(f, len, p);
+                        if (plausible_successor(f, len, p, h.idl, h.L))
+                            found = p; // positions rise within a lane: the last is the highest
+                    }
+                }
+            }
+        }
+        if (FWD) {
+            const uint64_t hit = __ballot(found != NONE);
+            if (hit) { // lanes hold increasing addresses: the lowest lane has the block's first candidate
+                const uint32_t l = (uint32_t)__builtin_ctzll(hit);
+                return ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(found >> 32), l) << 32) |
+                       __builtin_amdgcn_readlane((uint32_t)found, l);
+            }
+        }
+    }
+    if (FWD)
+        return NONE;
+    // highest over the wave (positions < 4 GiB: datafile offsets are u32)
+    uint32_t x = (uint32_t)found;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const uint32_t y = (uint32_t)__shfl_xor((int)x, o, 64);
+        x = y > x ? y : x;
+    }
+    return x;
+}
+
+// A1: speculative start of every chunk: the first entry header at or past the
+// chunk start c0 (one workgroup of NWS waves per chunk).  Half of the waves
+// search forward from c0 in interleaved SU-KiB blocks; the other half search
+// backward from c0 for the header of the entry that straddles it, whose end
+// is the answer.  A chunk start falls inside a payload far more often than
+// not (most bytes are in the large values), uniformly within it, so the
+// nearer of the two ends is found in half the scanning on average and in
+// the worst case.
+template <int NT, int SU>
+__global__ __launch_bounds__(NT) void walk_search_kernel(FileTab t, uint64_t *__restrict__ s_start,
+                                                         int32_t *__restrict__ s_status) {
+    constexpr uint32_t NWS = NT / 64, NF = NWS / 2, NB = NWS - NF;
     constexpr uint64_t SB = 1024u * SU; // bytes per wave block
-    __shared__ unsigned long long best;
+    __shared__ unsigned long long bestf;
+    __shared__ unsigned int bestb;
     const uint32_t lane = threadIdx.x & 63u, wid = threadIdx.x >> 6;
     const uint64_t w = blockIdx.x;
     const uint32_t fi = (uint32_t)(w / t.cpf), c = (uint32_t)(w % t.cpf);
@@ -244,64 +352,56 @@ __global__ __launch_bounds__(WALK_T) void walk_search_kernel(FileTab t, uint64_t
     }
     // positions p in [c0, c0 + C) with a whole 18-byte header in the file
     const uint64_t lim = (c0 + C < len - (ZDB_ENTRY_HEADER_SIZE - 1)) ? c0 + C : len - (ZDB_ENTRY_HEADER_SIZE - 1);
-    if (threadIdx.x == 0)
-        best = NONE;
+    constexpr uint64_t LO = ZDB_DATA_HEADER_SIZE; // entries start at or after the datafile header
+    if (threadIdx.x == 0) {
+        bestf = NONE;
+        bestb = 0u;
+    }
     __syncthreads();
-    for (uint64_t r0 = c0;; r0 += NWS * SB) {
-        const uint64_t b = r0 + wid * SB;
-        uint64_t found = NONE;
-        if (b < lim) {
-            uint4 a0[SU], a1[SU];
-#pragma unroll
-            for (int u = 0; u < SU; u++) { // every load of the block in flight
-                const uint64_t p0 = b + 1024u * u + 16u * lane; // 16-byte aligned (c0 is a multiple of C)
-                if (p0 < lim) {
-                    a0[u] = *reinterpret_cast<const uint4 *>(f + p0);
-                    a1[u] = *reinterpret_cast<const uint4 *>(f + p0 + 16);
-                } else {
-                    a0[u] = a1[u] = make_uint4(~0u, ~0u, ~0u, ~0u); // no candidate
-                }
+    bool back = true; // the backward search is still useful (block-uniform)
+    for (uint64_t k = 0;; k++) {
+        if (wid < NF) {
+            const uint64_t b = c0 + (k * NF + wid) * SB;
+            if (b < lim) {
+                const uint64_t found = scan_block<true, SU>(f, len, b, c0, lim, lane);
+                if (found != NONE && lane == 0)
+                    atomicMin(&bestf, (unsigned long long)found);
             }
-#pragma unroll
-            for (int u = 0; u < SU; u++) {
-                const uint64_t p0 = b + 1024u * u + 16u * lane;
-                const uint32_t d[8] = {a0[u].x, a0[u].y, a0[u].z, a0[u].w, a1[u].x, a1[u].y, a1[u].z, a1[u].w};
-                uint32_t z[4];
-                candidates(d, z);
-                uint64_t hit = 0;
-                if (z[0] | z[1] | z[2] | z[3]) { // rare: confirm through the successor's back-pointer
-#pragma unroll
-                    for (int j = 0; j < 4; j++) {
-                        uint32_t m = z[j];
-                        while (m && found == NONE) {
-                            const uint32_t r = (uint32_t)__builtin_ctz(m) >> 3;
-                            m &= ~(0xFFu << (8 * r));
-                            const uint64_t p = p0 + 4u * j + r;
-                            if (p < lim) {
-                                const Hdr h = load_hdr(f, len, p);
-                                if (plausible_successor(f, len, p, h.idl, h.L))
-                                    found = p;
-                            }
-                        }
-                    }
-                }
-                hit = __ballot(found != NONE);
-                if (hit) { // lanes hold increasing addresses: the lowest lane has the block's first candidate
-                    const uint32_t l = (uint32_t)__builtin_ctzll(hit);
-                    found = ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(found >> 32), l) << 32) |
-                            __builtin_amdgcn_readlane((uint32_t)found, l);
-                    break;
-                }
+        } else if (back) {
+            const uint64_t dist = (k * NB + (wid - NF) + 1) * SB; // block [c0 - dist, c0 - dist + SB)
+            if (dist < c0 + SB && c0 + SB - dist > LO) {
+                const uint64_t b = c0 > dist ? c0 - dist : 0;
+                const uint64_t found = scan_block<false, SU>(f, len, b, LO, c0, lane);
+                if (found && lane == 0)
+                    atomicMax(&bestb, (unsigned int)found);
             }
-            if (found != NONE && lane == 0)
-                atomicMin(&best, (unsigned long long)found);
         }
         __syncthreads();
-        const uint64_t bst = best;
+        const uint64_t bf = bestf;
+        const uint64_t bb = bestb;
         __syncthreads();
-        if (bst != NONE || r0 + NWS * SB >= lim) { // first block with a hit found, or the chunk is done
+        uint64_t ans = NONE;
+        bool done = false;
+        if (bf != NONE) { // the first header at or past c0
+            ans = bf;
+            done = true;
+        } else if (back && bb) { // the highest header before c0: its entry ends at the answer
+            const Hdr h = load_hdr(f, len, bb);
+            const uint64_t e = bb + ZDB_ENTRY_HEADER_SIZE + h.idl + h.L;
+            if (e >= c0) {
+                ans = e < lim ? e : NONE; // no entry starts in this chunk when it ends past it
+                done = true;
+            } else {
+                back = false; // not the straddling entry (a chain the filter cannot see): forward only
+            }
+        }
+        if (!done && c0 + (k + 1) * NF * SB >= lim)
+            done = true; // no header in [c0, lim)
+        if (back && (k + 1) * NB * SB >= c0 + SB - LO)
+            back = false; // reached the datafile header
+        if (done) {
             if (threadIdx.x == 0) {
-                s_start[w] = bst;
+                s_start[w] = ans;
                 s_status[w] = ST_CONTINUE;
             }
             return;
@@ -309,15 +409,16 @@ __global__ __launch_bounds__(WALK_T) void walk_search_kernel(FileTab t, uint64_t
     }
 }
 
-// A2: speculative chain of every chunk (one thread per chunk, 64 chains in
-// flight per wave); the first kcap records go to the chunk's slots so that an
-// accepted chunk is emitted by a parallel copy instead of a second walk
-__global__ __launch_bounds__(WALK_T) void walk_spec_kernel(FileTab t, const uint64_t *__restrict__ s_start,
-                                                           uint64_t *__restrict__ s_exit, uint32_t *__restrict__ s_count,
-                                                           int32_t *__restrict__ s_status, RecSlot *__restrict__ slots,
-                                                           uint32_t kcap) {
-    const uint64_t w = (uint64_t)blockIdx.x * WALK_T + threadIdx.x;
-    if (w >= (uint64_t)t.nfiles * t.cpf)
+// A2: speculative chain of every chunk (one lane per chunk, CHAINS_PER_WAVE
+// chains per one-wave workgroup); the first kcap records go to the chunk's
+// slots so that an accepted chunk is emitted by a parallel copy instead of a
+// second walk
+__global__ __launch_bounds__(64) void walk_spec_kernel(FileTab t, const uint64_t *__restrict__ s_start,
+                                                       uint64_t *__restrict__ s_exit, uint32_t *__restrict__ s_count,
+                                                       int32_t *__restrict__ s_status, RecSlot *__restrict__ slots,
+                                                       uint32_t kcap) {
+    const uint64_t w = (uint64_t)blockIdx.x * CHAINS_PER_WAVE + threadIdx.x;
+    if (threadIdx.x >= CHAINS_PER_WAVE || w >= (uint64_t)t.nfiles * t.cpf)
         return;
     const uint64_t start = s_start[w];
     if (start == NONE)
@@ -445,16 +546,16 @@ __global__ __launch_bounds__(WALK_T) void walk_copy_kernel(FileTab t, const uint
 }
 
 // C2: descriptors of the chunks that had to be re-walked, or had more
-// records than slots (one thread per chunk)
-__global__ __launch_bounds__(WALK_T) void walk_emit_kernel(FileTab t, const uint64_t *__restrict__ true_start,
-                                                           const uint32_t *__restrict__ chunk_mode,
-                                                           const uint64_t *__restrict__ chunk_base,
-                                                           const uint64_t *__restrict__ file_base, uint64_t capacity,
-                                                           uint64_t *__restrict__ entry_off, uint64_t *__restrict__ poff,
-                                                           uint32_t *__restrict__ plen,
-                                                           uint32_t *__restrict__ expect) {
-    const uint64_t w = (uint64_t)blockIdx.x * WALK_T + threadIdx.x;
-    if (w >= (uint64_t)t.nfiles * t.cpf || chunk_mode[w] != MODE_WALK)
+// records than slots (one lane per chunk, CHAINS_PER_WAVE per one-wave
+// workgroup, as A2)
+__global__ __launch_bounds__(64) void walk_emit_kernel(FileTab t, const uint64_t *__restrict__ true_start,
+                                                       const uint32_t *__restrict__ chunk_mode,
+                                                       const uint64_t *__restrict__ chunk_base,
+                                                       const uint64_t *__restrict__ file_base, uint64_t capacity,
+                                                       uint64_t *__restrict__ entry_off, uint64_t *__restrict__ poff,
+                                                       uint32_t *__restrict__ plen, uint32_t *__restrict__ expect) {
+    const uint64_t w = (uint64_t)blockIdx.x * CHAINS_PER_WAVE + threadIdx.x;
+    if (threadIdx.x >= CHAINS_PER_WAVE || w >= (uint64_t)t.nfiles * t.cpf || chunk_mode[w] != MODE_WALK)
         return;
     const uint32_t fi = (uint32_t)(w / t.cpf), c = (uint32_t)(w % t.cpf);
     const uint64_t cend = ((uint64_t)c + 1) << t.lg;
@@ -465,6 +566,16 @@ __global__ __launch_bounds__(WALK_T) void walk_emit_kernel(FileTab t, const uint
     walk_chain<EMIT>(t.image + foff, t.file_len[fi], true_start[w], cend, count, exit, st, nullptr, 0, foff,
                      file_base[fi] + chunk_base[w], capacity, entry_off, poff, plen, expect);
 }
+
+#ifdef ZDBCRC_DIAG
+int search_variant() {
+    static const int v = [] {
+        const char *e = std::getenv("ZDBCRC_SEARCH_VARIANT");
+        return e ? std::atoi(e) : 0;
+    }();
+    return v;
+}
+#endif
 
 // per (device, stream) workspace of the walk
 struct WalkWs {
@@ -535,9 +646,22 @@ int zdb_datafile_walk_device(const uint8_t *d_image, const uint64_t *d_file_off,
     RecSlot *slots = reinterpret_cast<RecSlot *>(b + 4 * al(nchunks * 8) + 3 * al(nchunks * 4));
 
     const FileTab t{d_image, d_file_off, d_file_len, nfiles, (uint32_t)cpf64, lg};
-    hipLaunchKernelGGL(walk_search_kernel, dim3((uint32_t)nchunks), dim3(WALK_T), 0, st, t, s_start, s_status);
-    const dim3 gch((uint32_t)((nchunks + WALK_T - 1) / WALK_T));
-    hipLaunchKernelGGL(walk_spec_kernel, gch, dim3(WALK_T), 0, st, t, s_start, s_exit, s_count, s_status, slots,
+#ifdef ZDBCRC_DIAG
+    switch (search_variant()) { // A/B (scripts/walk_probe.py with the diagnostic library)
+    case 1: hipLaunchKernelGGL((walk_search_kernel<128, 8>), dim3((uint32_t)nchunks), dim3(128), 0, st, t, s_start, s_status); break;
+    case 2: hipLaunchKernelGGL((walk_search_kernel<256, 16>), dim3((uint32_t)nchunks), dim3(256), 0, st, t, s_start, s_status); break;
+    case 3: hipLaunchKernelGGL((walk_search_kernel<512, 8>), dim3((uint32_t)nchunks), dim3(512), 0, st, t, s_start, s_status); break;
+    case 4: hipLaunchKernelGGL((walk_search_kernel<128, 16>), dim3((uint32_t)nchunks), dim3(128), 0, st, t, s_start, s_status); break;
+    case 5: hipLaunchKernelGGL((walk_search_kernel<512, 4>), dim3((uint32_t)nchunks), dim3(512), 0, st, t, s_start, s_status); break;
+    default:
+#endif
+    hipLaunchKernelGGL((walk_search_kernel<SEARCH_T, SEARCH_SU>), dim3((uint32_t)nchunks), dim3(SEARCH_T), 0, st, t,
+                       s_start, s_status);
+#ifdef ZDBCRC_DIAG
+    }
+#endif
+    const dim3 gchain((uint32_t)((nchunks + CHAINS_PER_WAVE - 1) / CHAINS_PER_WAVE));
+    hipLaunchKernelGGL(walk_spec_kernel, gchain, dim3(64), 0, st, t, s_start, s_exit, s_count, s_status, slots,
                        kcap);
     hipLaunchKernelGGL(walk_stitch_kernel, dim3((nfiles + WALK_T - 1) / WALK_T), dim3(WALK_T), 0, st, t, s_start,
                        s_exit, s_count, s_status, true_start, chunk_base, chunk_mode, kcap, d_file_records,
@@ -548,7 +672,7 @@ int zdb_datafile_walk_device(const uint8_t *d_image, const uint64_t *d_file_off,
         hipLaunchKernelGGL(walk_copy_kernel, dim3((uint32_t)((nslots + WALK_T - 1) / WALK_T)), dim3(WALK_T), 0, st,
                            t, chunk_mode, s_count, slots, kcap, chunk_base, d_file_records, capacity, d_entry_off,
                            d_payload_off, d_payload_len, d_expected);
-        hipLaunchKernelGGL(walk_emit_kernel, gch, dim3(WALK_T), 0, st, t, true_start, chunk_mode, chunk_base,
+        hipLaunchKernelGGL(walk_emit_kernel, gchain, dim3(64), 0, st, t, true_start, chunk_mode, chunk_base,
                            d_file_records, capacity, d_entry_off, d_payload_off, d_payload_len, d_expected);
     }
     return hipGetLastError() == hipSuccess ? ZDB_CRC32_OK : ZDB_CRC32_ELAUNCH;

@@ -67,17 +67,37 @@ def plausible_successor(f, ln, p, idl, L):
     return _le32(f, q + 5) == (p & 0xFFFFFFFF)
 
 
+SB, NF, NB = 8192, 2, 2  # search block bytes per wave, forward / backward waves per chunk
+
+
+def candidate(f, ln, p):
+    """filter: top byte of datalength 0 (L < 16 MiB; the writer caps at 8 MiB,
+    data.h:6), flags <= 3 (data.h:47-51), the entry's own `previous` before it
+    (data.c:601), then the successor's back-pointer"""
+    return (_byte(f, p + 4) == 0 and _byte(f, p + 13) <= MAXF and _le32(f, p + 5) < p
+            and plausible_successor(f, ln, p, int(f[p]), _le32(f, p + 1)))
+
+
 def search(f, ln, c0, C):
+    """the first entry header at or past c0, as walk_search_kernel finds it:
+    forward from c0 and backward from c0 (the header of the entry straddling
+    c0, whose end is the answer) in rounds of NF / NB blocks of SB bytes,
+    whichever direction hits in the earlier round (forward on a tie)"""
     if ln < 18:
         return NONE
     lim = min(c0 + C, ln - 17)
-    for p in range(c0, lim):
-        L = _le32(f, p + 1)
-        # filter: top byte of datalength 0 (L < 16 MiB; the writer caps at
-        # 8 MiB, data.h:6) and flags <= 3 (data.h:47-51)
-        if _byte(f, p + 4) == 0 and _byte(f, p + 13) <= MAXF and plausible_successor(f, ln, p, int(f[p]), L):
-            return p
-    return NONE
+    fwd = next((p for p in range(c0, lim) if candidate(f, ln, p)), NONE)
+    k_end = max(0, -(-(lim - c0) // (NF * SB)) - 1)  # the last forward round
+    rf = (fwd - c0) // (NF * SB) if fwd != NONE else None
+    kmax = k_end if rf is None else rf - 1  # the backward search decides only in an earlier round
+    lo = max(27, c0 - 1 - (kmax + 1) * NB * SB)
+    bwd = next((p for p in range(c0 - 1, lo, -1) if candidate(f, ln, p)), NONE) if kmax >= 0 else NONE
+    rb = ((c0 - 1 - bwd) // SB) // NB if bwd != NONE else None
+    if rb is not None and rb <= kmax:
+        e = bwd + 18 + int(f[bwd]) + _le32(f, bwd + 1)
+        if e >= c0:
+            return e if e < lim else NONE
+    return fwd
 
 
 def device_walk(f: np.ndarray, C: int, max_len: int | None = None):
