@@ -301,7 +301,9 @@ def verify_device(arena, offsets, lengths, expected, out, mismatch, count, strea
 
 
 def batch_host(arena: np.ndarray, offsets: np.ndarray, lengths: np.ndarray) -> np.ndarray:
-    """Host buffers in, host crcs out (H2D + kernel + D2H, synchronous)."""
+    """Host buffers in, host crcs out (synchronous).  An arena inside a
+    PinnedBuffer is read in place by the kernel (zero-copy), any other one is
+    staged; batches of at most 1,024 records return through the mailbox."""
     arena = np.ascontiguousarray(arena, dtype=np.uint8)
     offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
     lengths = np.ascontiguousarray(lengths, dtype=np.uint32)

@@ -507,6 +507,33 @@ def test_host_batch_zero_copy(dev, oracle_c, case):
         pin.free()
 
 
+def test_host_batch_mailbox_sizes_interleaved(dev, oracle_c):
+    """small host batches (at most 1,024 records) return through the mailbox,
+    whose device result buffer publish_kernel re-zeroes after each batch;
+    larger ones through a copy.  Batches of growing and shrinking size,
+    across the 1,024 boundary, pinned and pageable, with empty records and a
+    record that spans many waves, must all stay exact: a word left over from a
+    previous batch would show up as a wrong checksum in the next one"""
+    rng = np.random.default_rng(23)
+    total = 6 << 20
+    pin = dev.PinnedBuffer(total)
+    try:
+        pin.array[:total] = oracle.splitmix_bytes(total, 0x3A11)
+        plain = np.array(pin.array[:total])  # pageable copy: the staging path
+        for n in (1, 7, 1024, 3, 1025, 1024, 64, 4000, 2, 1):
+            lens = rng.integers(0, 3000, n)
+            lens[rng.random(n) < 0.1] = 0
+            if n == 3:
+                lens[1] = 5 << 20  # one record over many waves: cut partials XORed into out[]
+            offs = rng.integers(0, total - lens.max() - 1, n)
+            want = oracle_c.batch(plain, offs.astype(np.int64), lens.astype(np.int64))
+            for arena in (pin.array[:total], plain):
+                got = dev.batch_host(arena, offs.astype(np.uint64), lens.astype(np.uint32))
+                np.testing.assert_array_equal(got, want, err_msg=f"n={n}")
+    finally:
+        pin.free()
+
+
 @pytest.mark.parametrize("batch,datasize", [(1, 600_000), (64, 600_000), (4096, 256 << 20)])
 def test_set_pipeline_gpu_engine_matches_reference_daemon(tmp_path, batch, datasize):
     """f2: the two-phase SET batch with the GPU engine (values checksummed in
