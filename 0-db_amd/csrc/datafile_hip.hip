@@ -416,9 +416,9 @@ __global__ __launch_bounds__(NT) void walk_search_kernel(FileTab t, uint64_t *__
 __global__ __launch_bounds__(64) void walk_spec_kernel(FileTab t, const uint64_t *__restrict__ s_start,
                                                        uint64_t *__restrict__ s_exit, uint32_t *__restrict__ s_count,
                                                        int32_t *__restrict__ s_status, RecSlot *__restrict__ slots,
-                                                       uint32_t kcap) {
-    const uint64_t w = (uint64_t)blockIdx.x * CHAINS_PER_WAVE + threadIdx.x;
-    if (threadIdx.x >= CHAINS_PER_WAVE || w >= (uint64_t)t.nfiles * t.cpf)
+                                                       uint32_t kcap, uint32_t cpw) {
+    const uint64_t w = (uint64_t)blockIdx.x * cpw + threadIdx.x;
+    if (threadIdx.x >= cpw || w >= (uint64_t)t.nfiles * t.cpf)
         return;
     const uint64_t start = s_start[w];
     if (start == NONE)
@@ -553,9 +553,10 @@ __global__ __launch_bounds__(64) void walk_emit_kernel(FileTab t, const uint64_t
                                                        const uint64_t *__restrict__ chunk_base,
                                                        const uint64_t *__restrict__ file_base, uint64_t capacity,
                                                        uint64_t *__restrict__ entry_off, uint64_t *__restrict__ poff,
-                                                       uint32_t *__restrict__ plen, uint32_t *__restrict__ expect) {
-    const uint64_t w = (uint64_t)blockIdx.x * CHAINS_PER_WAVE + threadIdx.x;
-    if (threadIdx.x >= CHAINS_PER_WAVE || w >= (uint64_t)t.nfiles * t.cpf || chunk_mode[w] != MODE_WALK)
+                                                       uint32_t *__restrict__ plen, uint32_t *__restrict__ expect,
+                                                       uint32_t cpw) {
+    const uint64_t w = (uint64_t)blockIdx.x * cpw + threadIdx.x;
+    if (threadIdx.x >= cpw || w >= (uint64_t)t.nfiles * t.cpf || chunk_mode[w] != MODE_WALK)
         return;
     const uint32_t fi = (uint32_t)(w / t.cpf), c = (uint32_t)(w % t.cpf);
     const uint64_t cend = ((uint64_t)c + 1) << t.lg;
@@ -568,6 +569,15 @@ __global__ __launch_bounds__(64) void walk_emit_kernel(FileTab t, const uint64_t
 }
 
 #ifdef ZDBCRC_DIAG
+uint32_t chains_per_wave() { // A/B: ZDBCRC_CHAINS_PER_WAVE (1..64)
+    static const uint32_t v = [] {
+        const char *e = std::getenv("ZDBCRC_CHAINS_PER_WAVE");
+        const int x = e ? std::atoi(e) : 0;
+        return x >= 1 && x <= 64 ? (uint32_t)x : CHAINS_PER_WAVE;
+    }();
+    return v;
+}
+
 int search_variant() {
     static const int v = [] {
         const char *e = std::getenv("ZDBCRC_SEARCH_VARIANT");
@@ -660,9 +670,14 @@ int zdb_datafile_walk_device(const uint8_t *d_image, const uint64_t *d_file_off,
 #ifdef ZDBCRC_DIAG
     }
 #endif
-    const dim3 gchain((uint32_t)((nchunks + CHAINS_PER_WAVE - 1) / CHAINS_PER_WAVE));
+#ifdef ZDBCRC_DIAG
+    const uint32_t cpw = chains_per_wave();
+#else
+    const uint32_t cpw = CHAINS_PER_WAVE;
+#endif
+    const dim3 gchain((uint32_t)((nchunks + cpw - 1) / cpw));
     hipLaunchKernelGGL(walk_spec_kernel, gchain, dim3(64), 0, st, t, s_start, s_exit, s_count, s_status, slots,
-                       kcap);
+                       kcap, cpw);
     hipLaunchKernelGGL(walk_stitch_kernel, dim3((nfiles + WALK_T - 1) / WALK_T), dim3(WALK_T), 0, st, t, s_start,
                        s_exit, s_count, s_status, true_start, chunk_base, chunk_mode, kcap, d_file_records,
                        d_file_status, d_rewalks);
@@ -673,7 +688,7 @@ int zdb_datafile_walk_device(const uint8_t *d_image, const uint64_t *d_file_off,
                            t, chunk_mode, s_count, slots, kcap, chunk_base, d_file_records, capacity, d_entry_off,
                            d_payload_off, d_payload_len, d_expected);
         hipLaunchKernelGGL(walk_emit_kernel, gchain, dim3(64), 0, st, t, true_start, chunk_mode, chunk_base,
-                           d_file_records, capacity, d_entry_off, d_payload_off, d_payload_len, d_expected);
+                           d_file_records, capacity, d_entry_off, d_payload_off, d_payload_len, d_expected, cpw);
     }
     return hipGetLastError() == hipSuccess ? ZDB_CRC32_OK : ZDB_CRC32_ELAUNCH;
 }
