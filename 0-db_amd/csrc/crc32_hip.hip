@@ -442,7 +442,8 @@ __device__ __forceinline__ bool next_seg_batched(uint64_t &r, uint64_t n, uint64
         const uint64_t s_hi = ue < ur ? ue : ur;
         if (s_hi > s_lo) {
             const uint64_t A = readlane64(m.addr, li);
-            const uint64_t Aend = A + __builtin_amdgcn_readlane(m.len, li);
+            // (the builtin returns int: a length of 2 GiB or more must not be sign-extended)
+            const uint64_t Aend = A + (uint32_t)__builtin_amdgcn_readlane(m.len, li);
             sg.r = r;
             sg.us = us;
             sg.c.np = (uint32_t)(ur - us);
@@ -564,7 +565,7 @@ __device__ __forceinline__ uint64_t block_excl_scan64(uint64_t v, uint64_t *wsum
 // are flushed with atomic XOR at each claim (at most 2 are pending then).
 template <int WGT, int WPE, bool STAMP = false, int PRIO = 0, uint32_t UO = UNIT_OVH, int NOZ = 0,
           bool NTL = false, bool NOLOAD = false, int XM = 0, int DYN = 0, int CPW = 4, uint32_t DYN_POOLS = 8,
-          bool SP = false, int PP = 0>
+          bool SP = false, int PP = 0, bool SEGDUMP = false>
 __global__ __launch_bounds__(WGT, WPE) void crc_batch_kernel_v3(
     const uint8_t *__restrict__ arena, const uint64_t *__restrict__ offsets,
     const uint32_t *__restrict__ lengths, const PlanArgs plan, uint64_t n,
@@ -793,6 +794,13 @@ __global__ __launch_bounds__(WGT, WPE) void crc_batch_kernel_v3(
         uint32_t x = 0;                                                                                       \
         if (css + 1 == cur.S) {                                                                               \
             x = seg_value_v3<NOZ>(cur, acc, lane, lds, tables);                                               \
+            if (SEGDUMP && lane == 0) {                                                                       \
+                uint64_t *sd = reinterpret_cast<uint64_t *>(scratch + 16384) + 4 * gw;                        \
+                sd[0] = cur.c.pa;                                                                             \
+                sd[1] = cur.pb;                                                                               \
+                sd[2] = x;                                                                                    \
+                sd[3] = cur.r | ((uint64_t)cur.c.np << 32);                                                   \
+            }                                                                                                 \
             acc = 0;                                                                                          \
             if (cur.c.pa == 0 && cur.pb == cur.c.np) {                                                        \
                 dst = out + cur.r;                                                                            \
@@ -915,6 +923,8 @@ const KernelVariant kVariants[] = {
     {"v3_wg768_nt_dyn4c4p32_sp_pp_wait", crc_batch_kernel_v3<768, 6, false, 0, UNIT_OVH, false, true, false, 0, 4, 4, 32, true, 3>, 768},
     {"v3_wg768_nt_dyn4c4p32_sp_noz", crc_batch_kernel_v3<768, 6, false, 0, UNIT_OVH, 1, true, false, 0, 4, 4, 32, true>, 768},
     {"v3_wg768_nt_dyn4c4p32_sp_noz_noplace", crc_batch_kernel_v3<768, 6, false, 0, UNIT_OVH, 2, true, false, 0, 4, 4, 32, true>, 768},
+    // debugging: the default kernel writing each wave's last segment (pa, pb, value, r | np << 32)
+    {"v3_wg768_nt_dyn4c4p32_sp_segdump", crc_batch_kernel_v3<768, 6, false, 0, UNIT_OVH, false, true, false, 0, 4, 4, 32, true, 0, true>, 768},
 };
 constexpr int kNumVariants = (int)(sizeof(kVariants) / sizeof(kVariants[0]));
 std::atomic<int> g_variant{-1};

@@ -294,8 +294,8 @@ __device__ __forceinline__ uint64_t scan_block(const uint8_t *f, uint64_t len, u
             const uint64_t hit = __ballot(found != NONE);
             if (hit) { // lanes hold increasing addresses: the lowest lane has the block's first candidate
                 const uint32_t l = (uint32_t)__builtin_ctzll(hit);
-                return ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(found >> 32), l) << 32) |
-                       __builtin_amdgcn_readlane((uint32_t)found, l);
+                return ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)(found >> 32), l) << 32) |
+                       (uint32_t)__builtin_amdgcn_readlane((uint32_t)found, l); // int results: no sign extension
             }
         }
     }

@@ -48,6 +48,7 @@ VECTOR_SEED_BASE = 0x5EED0000
 C2_SEED = 0x5A0DB5EED
 C3_SEED = 0x5A0DB5EED + 3
 C3_LEN_SEED = 0xC3C3C3
+MAX_SEED = 0x5A0DB5EED + 9
 
 
 def kats(ref: oracle.Reference) -> list[dict]:
@@ -193,6 +194,7 @@ def digests(ref: oracle.Reference) -> dict:
                  **digest(ref, c3)}
     del arena
     out["C4"] = digest_c4(ref)
+    out["MAX"] = max_digest(ref)
     return out
 
 
@@ -208,6 +210,31 @@ def digest_c4(ref: oracle.Reference) -> dict:
     c4 = ref.batch(arena, lay["payload_off"].astype(np.uint64), lay["lens"].astype(np.uint32), threads=8)
     return {"seed": bench.C4_SEED, "len_seed": bench.C4_LEN_SEED, "files": len(lay["file_off"]),
             "image_bytes": lay["total"], "payload_bytes": int(lay["lens"].sum()), **digest(ref, c4)}
+
+
+def max_case() -> tuple[int, np.ndarray, np.ndarray]:
+    """the size limits of the interface on a 4.5 GiB arena: a record of the
+    largest length (2^32 - 1, u32), one of 0-db's largest payload (8 MiB,
+    data.h:6) past the 4 GiB offset mark, one straddling that mark, an empty
+    one, one ending at the arena's last byte, and 5,000 small ones beyond
+    4 GiB (tests/test_gpu.py::test_max_sizes_digest)"""
+    total = (9 << 29) + 1000
+    rng = np.random.default_rng(MAX_SEED)
+    offs = [100, (1 << 32) + 7, (1 << 32) - 8, (1 << 32) + 3, total - 4999]
+    lens = [(1 << 32) - 1, 8 << 20, 64, 0, 4999]
+    small = rng.integers(0, 70_000, 5000)
+    offs += [int(rng.integers(1 << 32, total - int(l))) for l in small]
+    lens += [int(l) for l in small]
+    return total, np.array(offs, np.uint64), np.array(lens, np.uint32)
+
+
+def max_digest(ref: oracle.Reference) -> dict:
+    import zdbcrc
+    total, offs, lens = max_case()
+    arena = zdbcrc.synth_fill(total, MAX_SEED)
+    crcs = ref.batch(arena, offs, lens, threads=8)
+    return {"seed": MAX_SEED, "total_bytes": total, "first": [f"{int(c):08x}" for c in crcs[:5]],
+            **digest(ref, crcs)}
 
 
 def c3_shard_digest(ref: oracle.Reference, rank: int, target: int) -> dict:
@@ -254,6 +281,12 @@ def main():
         d = json.loads((OUT / "digests.json").read_text())
         d.update(rank_digests(ref))
         (OUT / "digests.json").write_text(json.dumps(d, indent=1) + "\n")
+        return
+    if "--only-max" in sys.argv:  # add / refresh the size-limit digest only
+        d = json.loads((OUT / "digests.json").read_text())
+        d["MAX"] = max_digest(ref)
+        (OUT / "digests.json").write_text(json.dumps(d, indent=1) + "\n")
+        print("digests.json MAX:", d["MAX"])
         return
     if "--only-c4" in sys.argv:  # add / refresh the C4 digest only
         d = json.loads((OUT / "digests.json").read_text())

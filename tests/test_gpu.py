@@ -4,6 +4,7 @@ work).  Run on an MI355X with `pytest -m gpu`."""
 from __future__ import annotations
 
 import os
+import sys
 import shutil
 import subprocess
 from pathlib import Path
@@ -224,6 +225,30 @@ def test_full_size_c3_digest(dev, oracle_c, digests):
     torch.cuda.synchronize()
     got = _digest(oracle_c.crc32, out.cpu().numpy().view(np.uint32))
     assert got == {k: d[k] for k in ("count", "xor", "crc_of_crcs")}
+
+
+def test_max_sizes_digest(dev, oracle_c, digests):
+    """The interface's size limits on a 4.5 GiB device arena: one record of
+    2^32 - 1 bytes (the largest u32 length: every wave of the grid cuts it,
+    the tail pool is off for it), an 8 MiB payload past the 4 GiB offset mark,
+    a record straddling that mark, an empty one, one ending at the arena's
+    last byte, 5,000 small ones beyond 4 GiB -- against the reference's crcs
+    (tests/golden/make_golden.py --only-max, pinned by the oracle as well)"""
+    sys.path.insert(0, str(GOLDEN))
+    from make_golden import max_case
+    d = digests["MAX"]
+    total, offs, lens = max_case()
+    assert total == d["total_bytes"]
+    arena = torch.empty(total + 64, dtype=torch.uint8, device="cuda")
+    dev.synth_fill_device(arena[:total], d["seed"])
+    out = torch.empty(len(lens), dtype=torch.int32, device="cuda")
+    dev.batch_device(arena, torch.from_numpy(offs.view(np.int64)).cuda(),
+                     torch.from_numpy(lens.view(np.int32)).cuda(), out)
+    torch.cuda.synchronize()
+    crcs = out.cpu().numpy().view(np.uint32)
+    assert [f"{int(c):08x}" for c in crcs[:5]] == d["first"]
+    assert _digest(oracle_c.crc32, crcs) == {k: d[k] for k in ("count", "xor", "crc_of_crcs")}
+    del arena
 
 
 def test_repeat_is_deterministic(dev):
