@@ -182,3 +182,24 @@ def test_device_scan_c4_shaped_store(dev):
     st.scan(1 << 20)
     cnt = int(st.mismatch_count.cpu()[0])
     assert sorted(st.mismatch[:cnt].cpu().numpy().tolist()) == hit
+
+
+def test_device_scan_files_over_2GiB(dev):
+    """two C4-shaped datafiles of ~3 GiB each (entry offsets past 2^31, the
+    top of a datafile's u32 offsets in reach): the walk finds exactly the
+    layout's entries with every chunk speculated right, and the scan matches
+    every stored crc"""
+    sys.path.insert(0, str(ROOT))
+    import bench
+    lay = bench.c4_layout(5, files=2, file_cap=3 << 30)
+    assert lay["file_size"].max() > (5 << 29)  # positions beyond 2.5 GiB in both files
+    img, _, _, _, crcs = bench.c4_build_device(lay, 0x2B16)
+    st = dev.DeviceStore(img, lay["file_off"], lay["file_size"], capacity=len(crcs) + 10)
+    n = st.scan()
+    assert n == len(crcs)
+    np.testing.assert_array_equal(st.entry_off[:n].cpu().numpy(), lay["entry_off"])
+    assert (st.file_status.cpu().numpy() == 0).all()
+    assert int(st.rewalks.cpu()[-1]) == 0
+    assert int(st.mismatch_count.cpu()[0]) == 0
+    np.testing.assert_array_equal(st.computed[:n].cpu().numpy().view(np.uint32), crcs)
+    del img, st
