@@ -203,3 +203,22 @@ def test_device_scan_files_over_2GiB(dev):
     assert int(st.mismatch_count.cpu()[0]) == 0
     np.testing.assert_array_equal(st.computed[:n].cpu().numpy().view(np.uint32), crcs)
     del img, st
+
+
+@pytest.mark.parametrize("chunk", [1024, 4096])
+def test_device_scan_many_small_chunks(dev, chunk):
+    """16 C4-shaped datafiles of 8 MiB walked in 1 KiB / 4 KiB chunks: more
+    than 65,536 chunks at 1 KiB (the walk then keeps 64 record slots per
+    chunk instead of 512, and overfull chunks are emitted by a second walk)"""
+    sys.path.insert(0, str(ROOT))
+    import bench
+    lay = bench.c4_layout(6, files=16, file_cap=8 << 20)
+    img, _, _, _, crcs = bench.c4_build_device(lay, 0x1C)
+    st = dev.DeviceStore(img, lay["file_off"], lay["file_size"], capacity=len(crcs) + 10)
+    n = st.scan(chunk)
+    assert n == len(crcs)
+    np.testing.assert_array_equal(st.entry_off[:n].cpu().numpy(), lay["entry_off"])
+    np.testing.assert_array_equal(st.payload_off[:n].cpu().numpy(), lay["payload_off"])
+    assert (st.file_status.cpu().numpy() == 0).all()
+    assert int(st.mismatch_count.cpu()[0]) == 0
+    np.testing.assert_array_equal(st.computed[:n].cpu().numpy().view(np.uint32), crcs)
