@@ -65,7 +65,10 @@ constexpr int32_t ST_CONTINUE = -1;
 // follow longer chains
 constexpr uint32_t DEFAULT_LG_CHUNK = 23;
 constexpr uint32_t WALK_T = 256;
-constexpr int SEARCH_T = 256, SEARCH_SU = 8; // search: threads per chunk, KiB per wave block
+// search: threads per chunk, KiB per wave block; each lane loads its own 16
+// bytes only and takes the next 16 from its neighbour (walk 0.58 -> 0.51 ms
+// on C4, profiles/r2/walk_search_ab*.jsonl)
+constexpr int SEARCH_T = 256, SEARCH_SU = 8;
 // chains per wave (A2, C2): the lanes of a wave hop in lockstep, each hop
 // waiting for the slowest of its lanes' header loads, so fewer chains per
 // wave on more CUs shorten every hop
@@ -246,25 +249,58 @@ __device__ __forceinline__ void candidates(const uint32_t (&d)[8], uint32_t (&z)
 // if none).  Wave-uniform result.  Loads read [p0, p0 + 32) for every lane
 // whose 16 positions meet [lo, hi) (p0 >= 16 whenever lo >= 28, and at most 32
 // bytes past hi: within the file, or within the 16 readable bytes past it)
-template <bool FWD, int SU>
+// NOA1: each lane loads its own 16 bytes only and takes the following 16
+// from the next lane (DPP wave shift; lane 63 from lane 0 of the next 1 KiB,
+// or from one extra load after the block)
+__device__ __forceinline__ uint32_t from_next_lane(uint32_t own_next_row0, uint32_t v, uint32_t lane) {
+    const uint32_t sh = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x130, 0xF, 0xF, false); // wave_shl:1
+    return lane == 63 ? own_next_row0 : sh;
+}
+
+template <bool FWD, int SU, bool NOA1 = false>
 __device__ __forceinline__ uint64_t scan_block(const uint8_t *f, uint64_t len, uint64_t b, uint64_t lo, uint64_t hi,
                                                uint32_t lane) {
-    uint4 a0[SU], a1[SU];
+    uint4 a0[SU], a1[NOA1 ? 1 : SU], tl = make_uint4(~0u, ~0u, ~0u, ~0u);
 #pragma unroll
     for (int u = 0; u < SU; u++) { // every load of the block in flight
         const uint64_t p0 = b + 1024u * u + 16u * lane;
-        if (p0 + 16 > lo && p0 < hi) {
+        if (NOA1) { // also the 16 bytes the previous lane's positions need
+            a0[u] = p0 + 32 > lo && p0 < hi + 16 ? *reinterpret_cast<const uint4 *>(f + p0)
+                                                  : make_uint4(~0u, ~0u, ~0u, ~0u);
+        } else if (p0 + 16 > lo && p0 < hi) {
             a0[u] = *reinterpret_cast<const uint4 *>(f + p0);
             a1[u] = *reinterpret_cast<const uint4 *>(f + p0 + 16);
         } else {
             a0[u] = a1[u] = make_uint4(~0u, ~0u, ~0u, ~0u); // no candidate
         }
     }
+    // the 16 bytes after the block, for lane 63 of the last row.  The address
+    // is wave-uniform and not 4-byte aligned in general (files sit at any
+    // offset of the image): it must stay a vector load -- as a scalar load
+    // (which the compiler chose in the 128-thread shape) the low address
+    // bits are dropped and the bytes are wrong (walk_search_ab3-5)
+    if (NOA1 && b + 1024u * SU < hi + 16) {
+        uint64_t ta = reinterpret_cast<uint64_t>(f + b + 1024u * SU);
+        __asm__ volatile("" : "+v"(ta)); // keep the address in a VGPR
+        tl = *reinterpret_cast<const uint4 *>(ta);
+    }
     uint64_t found = FWD ? NONE : 0;
 #pragma unroll
     for (int u = 0; u < SU; u++) {
         const uint64_t p0 = b + 1024u * u + 16u * lane;
-        const uint32_t d[8] = {a0[u].x, a0[u].y, a0[u].z, a0[u].w, a1[u].x, a1[u].y, a1[u].z, a1[u].w};
+        uint4 nx;
+        if (NOA1) {
+            const uint4 r0 = u + 1 < SU ? make_uint4(__builtin_amdgcn_readlane(a0[u + 1 < SU ? u + 1 : u].x, 0),
+                                                     __builtin_amdgcn_readlane(a0[u + 1 < SU ? u + 1 : u].y, 0),
+                                                     __builtin_amdgcn_readlane(a0[u + 1 < SU ? u + 1 : u].z, 0),
+                                                     __builtin_amdgcn_readlane(a0[u + 1 < SU ? u + 1 : u].w, 0))
+                                        : tl;
+            nx = make_uint4(from_next_lane(r0.x, a0[u].x, lane), from_next_lane(r0.y, a0[u].y, lane),
+                            from_next_lane(r0.z, a0[u].z, lane), from_next_lane(r0.w, a0[u].w, lane));
+        } else {
+            nx = a1[NOA1 ? 0 : u];
+        }
+        const uint32_t d[8] = {a0[u].x, a0[u].y, a0[u].z, a0[u].w, nx.x, nx.y, nx.z, nx.w};
         uint32_t z[4];
         candidates(d, z);
         if (z[0] | z[1] | z[2] | z[3]) { // rare: confirm through the successor's back-pointer
@@ -319,7 +355,7 @@ __device__ __forceinline__ uint64_t scan_block(const uint8_t *f, uint64_t len, u
 // not (most bytes are in the large values), uniformly within it, so the
 // nearer of the two ends is found in half the scanning on average and in
 // the worst case.
-template <int NT, int SU>
+template <int NT, int SU, bool NOA1 = false>
 __global__ __launch_bounds__(NT) void walk_search_kernel(FileTab t, uint64_t *__restrict__ s_start,
                                                          int32_t *__restrict__ s_status) {
     constexpr uint32_t NWS = NT / 64, NF = NWS / 2, NB = NWS - NF;
@@ -363,7 +399,7 @@ __global__ __launch_bounds__(NT) void walk_search_kernel(FileTab t, uint64_t *__
         if (wid < NF) {
             const uint64_t b = c0 + (k * NF + wid) * SB;
             if (b < lim) {
-                const uint64_t found = scan_block<true, SU>(f, len, b, c0, lim, lane);
+                const uint64_t found = scan_block<true, SU, NOA1>(f, len, b, c0, lim, lane);
                 if (found != NONE && lane == 0)
                     atomicMin(&bestf, (unsigned long long)found);
             }
@@ -371,7 +407,7 @@ __global__ __launch_bounds__(NT) void walk_search_kernel(FileTab t, uint64_t *__
             const uint64_t dist = (k * NB + (wid - NF) + 1) * SB; // block [c0 - dist, c0 - dist + SB)
             if (dist < c0 + SB && c0 + SB - dist > LO) {
                 const uint64_t b = c0 > dist ? c0 - dist : 0;
-                const uint64_t found = scan_block<false, SU>(f, len, b, LO, c0, lane);
+                const uint64_t found = scan_block<false, SU, NOA1>(f, len, b, LO, c0, lane);
                 if (found && lane == 0)
                     atomicMax(&bestb, (unsigned int)found);
             }
@@ -569,6 +605,11 @@ __global__ __launch_bounds__(64) void walk_emit_kernel(FileTab t, const uint64_t
 }
 
 #ifdef ZDBCRC_DIAG
+struct LastWalk {
+    uint8_t *ws;
+    uint64_t nchunks;
+} g_last_walk = {nullptr, 0};
+
 uint32_t chains_per_wave() { // A/B: ZDBCRC_CHAINS_PER_WAVE (1..64)
     static const uint32_t v = [] {
         const char *e = std::getenv("ZDBCRC_CHAINS_PER_WAVE");
@@ -646,6 +687,9 @@ int zdb_datafile_walk_device(const uint8_t *d_image, const uint64_t *d_file_off,
         ws.bytes = need;
     }
     uint8_t *b = static_cast<uint8_t *>(ws.ptr);
+#ifdef ZDBCRC_DIAG
+    g_last_walk = {b, nchunks};
+#endif
     uint64_t *s_start = reinterpret_cast<uint64_t *>(b);
     uint64_t *s_exit = reinterpret_cast<uint64_t *>(b + al(nchunks * 8));
     uint64_t *true_start = reinterpret_cast<uint64_t *>(b + 2 * al(nchunks * 8));
@@ -658,15 +702,19 @@ int zdb_datafile_walk_device(const uint8_t *d_image, const uint64_t *d_file_off,
     const FileTab t{d_image, d_file_off, d_file_len, nfiles, (uint32_t)cpf64, lg};
 #ifdef ZDBCRC_DIAG
     switch (search_variant()) { // A/B (scripts/walk_probe.py with the diagnostic library)
+    case 9: hipLaunchKernelGGL((walk_search_kernel<256, 8, false>), dim3((uint32_t)nchunks), dim3(256), 0, st, t, s_start, s_status); break;
     case 1: hipLaunchKernelGGL((walk_search_kernel<128, 8>), dim3((uint32_t)nchunks), dim3(128), 0, st, t, s_start, s_status); break;
     case 2: hipLaunchKernelGGL((walk_search_kernel<256, 16>), dim3((uint32_t)nchunks), dim3(256), 0, st, t, s_start, s_status); break;
     case 3: hipLaunchKernelGGL((walk_search_kernel<512, 8>), dim3((uint32_t)nchunks), dim3(512), 0, st, t, s_start, s_status); break;
     case 4: hipLaunchKernelGGL((walk_search_kernel<128, 16>), dim3((uint32_t)nchunks), dim3(128), 0, st, t, s_start, s_status); break;
     case 5: hipLaunchKernelGGL((walk_search_kernel<512, 4>), dim3((uint32_t)nchunks), dim3(512), 0, st, t, s_start, s_status); break;
+    case 6: hipLaunchKernelGGL((walk_search_kernel<256, 8, true>), dim3((uint32_t)nchunks), dim3(256), 0, st, t, s_start, s_status); break;
+    case 7: hipLaunchKernelGGL((walk_search_kernel<256, 16, true>), dim3((uint32_t)nchunks), dim3(256), 0, st, t, s_start, s_status); break;
+    case 8: hipLaunchKernelGGL((walk_search_kernel<128, 16, true>), dim3((uint32_t)nchunks), dim3(128), 0, st, t, s_start, s_status); break;
     default:
 #endif
-    hipLaunchKernelGGL((walk_search_kernel<SEARCH_T, SEARCH_SU>), dim3((uint32_t)nchunks), dim3(SEARCH_T), 0, st, t,
-                       s_start, s_status);
+    hipLaunchKernelGGL((walk_search_kernel<SEARCH_T, SEARCH_SU, true>), dim3((uint32_t)nchunks), dim3(SEARCH_T), 0,
+                       st, t, s_start, s_status);
 #ifdef ZDBCRC_DIAG
     }
 #endif
@@ -692,6 +740,22 @@ int zdb_datafile_walk_device(const uint8_t *d_image, const uint64_t *d_file_off,
     }
     return hipGetLastError() == hipSuccess ? ZDB_CRC32_OK : ZDB_CRC32_ELAUNCH;
 }
+
+#ifdef ZDBCRC_DIAG
+// measurement/debug hook: the speculative and the true start of every chunk
+// of the last walk (device arrays copied to host; NONE = ~0)
+int zdbcrc_debug_walk_starts(uint64_t *s_start, uint64_t *true_start, uint64_t nchunks) {
+    if (!g_last_walk.ws || nchunks != g_last_walk.nchunks)
+        return -1;
+    auto al = [](size_t x) { return (x + 255) & ~size_t(255); };
+    const uint8_t *b = g_last_walk.ws;
+    if (hipDeviceSynchronize() != hipSuccess ||
+        hipMemcpy(s_start, b, nchunks * 8, hipMemcpyDeviceToHost) != hipSuccess ||
+        hipMemcpy(true_start, b + 2 * al(nchunks * 8), nchunks * 8, hipMemcpyDeviceToHost) != hipSuccess)
+        return -1;
+    return 0;
+}
+#endif
 
 int zdb_datafile_scan_device(const uint8_t *d_image, const uint64_t *d_file_off, const uint64_t *d_file_len,
                              uint32_t nfiles, uint64_t max_file_len, uint32_t chunk_bytes,
