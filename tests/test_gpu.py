@@ -164,6 +164,35 @@ def test_verify_reports_mismatches(dev, oracle_c):
     np.testing.assert_array_equal(out.cpu().numpy().view(np.uint32), exp)
 
 
+def test_verify_more_mismatches_than_room(dev, oracle_c):
+    """more mismatching records (300) than the mismatch list holds (16): the
+    count is the full count, the list holds 16 distinct mismatching indices,
+    and nothing is written past it"""
+    arena = oracle.splitmix_bytes(400_000, 21)
+    rng = np.random.default_rng(21)
+    lens = rng.integers(0, 3000, 5000)
+    offs = np.array([rng.integers(0, 400_000 - l) for l in lens])
+    exp = oracle_c.batch(arena, offs, lens)
+    bad = np.sort(rng.choice(5000, 300, replace=False))
+    exp_t = exp.copy()
+    exp_t[bad] ^= 0x80000000
+    a = torch.from_numpy(arena).cuda()
+    o = torch.from_numpy(offs.astype(np.int64)).cuda()
+    l = torch.from_numpy(lens.astype(np.int32)).cuda()
+    e = torch.from_numpy(exp_t.view(np.int32)).cuda()
+    out = torch.zeros(5000, dtype=torch.int32, device="cuda")
+    guard = torch.full((32,), -7, dtype=torch.int32, device="cuda")
+    mism = guard[:16]
+    cnt = torch.zeros(1, dtype=torch.int32, device="cuda")
+    dev.verify_device(a, o, l, e, out, mism, cnt)
+    torch.cuda.synchronize()
+    assert int(cnt.item()) == 300
+    listed = guard[:16].cpu().numpy()
+    assert len(set(listed.tolist())) == 16 and set(listed.tolist()) <= set(bad.tolist())
+    assert (guard[16:].cpu().numpy() == -7).all()
+    np.testing.assert_array_equal(out.cpu().numpy().view(np.uint32), exp)
+
+
 def test_host_buffer_api(dev, oracle_c):
     arena = oracle.splitmix_bytes(1 << 20, 14)
     rng = np.random.default_rng(14)
