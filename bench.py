@@ -504,6 +504,7 @@ def e2e_legs(offs, lens, seed) -> dict:
                 "auto_engine_tool_jobs8": ([[tool, "--engine=auto", "--jobs=8"] + files], 8),
                 "scalar_engine_tool_jobs8": ([[tool, "--engine=cpu", "--jobs=8"] + files], 8),
                 "gpu_tool_jobs8_32files": ([[tool, "--jobs=8"] + files32], 32),
+                "auto_engine_tool_jobs8_32files": ([[tool, "--engine=auto", "--jobs=8"] + files32], 32),
                 "scalar_engine_tool_jobs8_32files": ([[tool, "--engine=cpu", "--jobs=8"] + files32], 32)}
         if oracle.REF_INTEGRITY.exists():
             runs["reference_tool_per_file"] = ([[str(oracle.REF_INTEGRITY), f] for f in files], 8)
