@@ -372,6 +372,55 @@ def test_tool_gpu_256MiB_matches_reference(big_datafile, engine):
     assert p.stderr == ref.stderr
 
 
+@pytest.fixture(scope="module", params=["max8MiB", "zipf160MiB"])
+def large_value_datafile(request, tmp_path_factory):
+    """reference-written datafiles of large values: 24 values of exactly
+    ZDB_DATA_MAX_PAYLOAD (libzdb/data.h:6, 8 MiB) and a 160 MiB SURVEY §8(d)
+    C3 mix (up to 1 MiB per value); payload bytes flipped at the first byte,
+    the last byte and inside of several values, including the largest; the
+    reference integrity-check's output on each"""
+    if not (oracle.REF_GEN.exists() and oracle.REF_INTEGRITY.exists()):
+        pytest.skip("oracle/_ref not built")
+    d = tmp_path_factory.mktemp(request.param)
+    if request.param == "max8MiB":
+        args = ["fixed", "24", "7", str(8 << 20)]
+    else:
+        args = ["zipf", "1000000", "8", str(160 << 20)]
+    subprocess.run([str(oracle.REF_GEN), str(d), *args], check=True, capture_output=True)
+    d0 = d / "data" / "default" / "d0"
+    img = bytearray(d0.read_bytes())
+    import zdbcrc
+    recs, _ = zdbcrc.datafile_walk(bytes(img))
+    off = recs["payload_offset"].astype(np.int64)
+    ln = recs["datalength"].astype(np.int64)
+    big = int(np.argmax(ln))
+    flips = {0: 0, big: int(ln[big]) - 1, len(ln) // 2: int(ln[len(ln) // 2]) // 2,
+             len(ln) - 1: int(ln[-1]) - 1}
+    for k, at in flips.items():
+        img[int(off[k]) + at] ^= 0x40
+    d0.write_bytes(bytes(img))
+    os.symlink("d0", d / "data" / "default" / "zdb-data-0")
+    p = subprocess.run([str(oracle.REF_INTEGRITY), str(d / "data" / "default" / "zdb-data-0")], capture_output=True,
+                       env=dict(os.environ, TZ="UTC"), timeout=120)
+    assert p.returncode == len(flips)  # the tool exits with its error count
+    return d / "data" / "default" / "zdb-data-0", p
+
+
+@pytest.mark.parametrize("engine", ["hip", "auto"])
+def test_tool_gpu_large_values_match_reference(large_value_datafile, engine):
+    """the GPU tool on 8 MiB (maximum) and Zipf-mixed values: the reference
+    tool's stdout, stderr and exit status"""
+    import re
+    path, ref = large_value_datafile
+    from test_tool_cpu import TOOL
+    p = subprocess.run([str(TOOL), f"--engine={engine}", str(path)], capture_output=True,
+                       env=dict(os.environ, TZ="UTC"), timeout=120)
+    t = re.compile(rb"\[\s*\d+\.\d{6}\]")
+    assert p.returncode == ref.returncode
+    assert t.sub(b"[T]", p.stdout) == t.sub(b"[T]", ref.stdout)
+    assert p.stderr == ref.stderr
+
+
 @pytest.mark.parametrize("jobs", [1, 3])
 def test_tool_gpu_multi_file_scan(tmp_path, datafile_cases, jobs):
     """several datafiles in one run, worker threads sharing the GPU: every
