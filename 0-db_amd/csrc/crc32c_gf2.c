@@ -131,37 +131,62 @@ static uint32_t reg_slice(uint32_t v, int c) {
     return (uint32_t)(((uint64_t)v << (5 * c)) & 0xFFFFFFFFu);
 }
 
+/* dst[v * stride] for v < 32 from the images of the 5 unit vectors: every
+ * table below is GF(2)-linear in v, so one XOR per entry replaces a multiply */
+static void fill_linear(uint32_t *dst, size_t stride, const uint32_t basis[5]) {
+    dst[0] = 0;
+    for (uint32_t v = 1; v < 32; v++) {
+        const int t = __builtin_ctz(v);
+        dst[v * stride] = dst[(v & (v - 1)) * stride] ^ basis[t];
+    }
+}
+
 void zdbcrc_build_tables(uint32_t *img) {
     gf2_ready();
     memset(img, 0, sizeof(uint32_t) * ZDBCRC_TABLE_DW);
+    uint32_t b[5];
 
-    for (int i = 0; i < ZDBCRC_K; i++)
-        for (int c = 0; c < ZDBCRC_PCH; c++)
-            for (uint32_t v = 0; v < 32; v++)
-                img[ZDBCRC_OFF_T + (i * ZDBCRC_PCH + c) * 32 + v] =
-                    zdbcrc_shift(piece_window_crc(v, c), 1024 * (int64_t)(ZDBCRC_K - 1 - i));
+    for (int i = 0; i < ZDBCRC_K; i++) {
+        const uint32_t m = xpow(8 * 1024 * (uint64_t)(ZDBCRC_K - 1 - i), 0);
+        for (int c = 0; c < ZDBCRC_PCH; c++) {
+            for (int t = 0; t < 5; t++)
+                b[t] = multmodp(m, piece_window_crc(1u << t, c));
+            fill_linear(img + ZDBCRC_OFF_T + (i * ZDBCRC_PCH + c) * 32, 1, b);
+        }
+    }
 
-    for (int c = 0; c < ZDBCRC_SCH; c++)
-        for (uint32_t v = 0; v < 32; v++)
-            img[ZDBCRC_OFF_W + c * 32 + v] = zdbcrc_shift(reg_slice(v, c), 1024 * ZDBCRC_K);
+    const uint32_t mw = xpow(8 * 1024 * (uint64_t)ZDBCRC_K, 0);
+    for (int c = 0; c < ZDBCRC_SCH; c++) {
+        for (int t = 0; t < 5; t++)
+            b[t] = multmodp(mw, reg_slice(1u << t, c));
+        fill_linear(img + ZDBCRC_OFF_W + c * 32, 1, b);
+    }
 
-    for (int c = 0; c < ZDBCRC_SCH; c++)
-        for (uint32_t v = 0; v < 32; v++)
-            for (int l = 0; l < ZDBCRC_WAVE; l++)
-                img[ZDBCRC_OFF_L + (c * 32 + v) * ZDBCRC_WAVE + l] =
-                    zdbcrc_shift(reg_slice(v, c), 16 * (int64_t)(ZDBCRC_WAVE - 1 - l));
+    for (int l = 0; l < ZDBCRC_WAVE; l++) {
+        const uint32_t m = xpow(8 * 16 * (uint64_t)(ZDBCRC_WAVE - 1 - l), 0);
+        for (int c = 0; c < ZDBCRC_SCH; c++) {
+            for (int t = 0; t < 5; t++)
+                b[t] = multmodp(m, reg_slice(1u << t, c));
+            fill_linear(img + ZDBCRC_OFF_L + c * 32 * ZDBCRC_WAVE + l, ZDBCRC_WAVE, b);
+        }
+    }
 
-    for (int z = 0; z < 16; z++)
-        for (int c = 0; c < ZDBCRC_SCH; c++)
-            for (uint32_t v = 0; v < 32; v++)
-                img[ZDBCRC_OFF_Z + (z * ZDBCRC_SCH + c) * 32 + v] = zdbcrc_shift(reg_slice(v, c), -z);
+    for (int z = 0; z < 16; z++) {
+        const uint32_t m = xpow(8 * (uint64_t)z, 1);
+        for (int c = 0; c < ZDBCRC_SCH; c++) {
+            for (int t = 0; t < 5; t++)
+                b[t] = multmodp(m, reg_slice(1u << t, c));
+            fill_linear(img + ZDBCRC_OFF_Z + (z * ZDBCRC_SCH + c) * 32, 1, b);
+        }
+    }
 
     for (int j = 0; j < ZDBCRC_RDIG; j++)
         for (uint32_t d = 0; d < 256; d++) {
             const uint32_t m = xpow((uint64_t)d << (8 * j + 7), 0); /* x^(8 * 16 * d * 256^j) */
-            for (int c = 0; c < ZDBCRC_SCH; c++)
-                for (uint32_t v = 0; v < 32; v++)
-                    img[ZDBCRC_OFF_R + ((j * 256 + d) * ZDBCRC_SCH + c) * 32 + v] =
-                        multmodp(m, reg_slice(v, c));
+            for (int c = 0; c < ZDBCRC_SCH; c++) {
+                for (int t = 0; t < 5; t++)
+                    b[t] = multmodp(m, reg_slice(1u << t, c));
+                fill_linear(img + ZDBCRC_OFF_R + ((j * 256 + d) * ZDBCRC_SCH + c) * 32, 1, b);
+            }
         }
 }

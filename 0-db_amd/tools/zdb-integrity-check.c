@@ -250,6 +250,7 @@ static int g_gpu_count = 0;
 static int g_gpu_devices = 0; /* devices the workers are spread over */
 static pthread_mutex_t g_gpu_mu = PTHREAD_MUTEX_INITIALIZER;
 static pthread_cond_t g_gpu_cv = PTHREAD_COND_INITIALIZER;
+static double g_gpu_t0, g_gpu_t_count, g_gpu_t_up; /* start-up thread timeline (--trace) */
 
 #define ENGINE_CPU 0
 #define ENGINE_HIP 1
@@ -307,7 +308,9 @@ static int load_gpu(void) {
  * workers read their files */
 static void *gpu_init_main(void *arg) {
     const int want = *(const int *)arg;
+    g_gpu_t0 = now_s();
     int ok = load_gpu();
+    g_gpu_t_count = now_s();
     if (ok) {
         g_gpu_devices = want > 0 && want < g_gpu_count ? want : g_gpu_count;
         for (int d = 0; ok && d < g_gpu_devices; d++) {
@@ -318,6 +321,7 @@ static void *gpu_init_main(void *arg) {
         }
     }
     pthread_mutex_lock(&g_gpu_mu);
+    g_gpu_t_up = now_s();
     g_gpu_ok = ok;
     pthread_cond_broadcast(&g_gpu_cv);
     pthread_mutex_unlock(&g_gpu_mu);
@@ -537,12 +541,16 @@ static void check_file(const config_t *cfg, worker_t *w, const char *filename, r
     int errors = 0;
     const double t_sum = now_s();
     const char *engine_used = "none";
+    double gpu_wait_ms = 0;
     if (m) {
         /* hip: always the GPU (waiting for it to come up); auto: the GPU if
          * it is up by now, the scalar engine otherwise */
         int use_gpu = 0;
         if (cfg->engine == ENGINE_HIP) {
-            if (gpu_state(1) != 1) {
+            const double t_wait = now_s();
+            const int up = gpu_state(1);
+            gpu_wait_ms = (now_s() - t_wait) * 1e3;
+            if (up != 1) {
                 rep_err(r, "[-] zdb-integrity-check: GPU engine unavailable (use --engine=cpu)\n");
                 r->status = FATAL_EXIT | EXIT_FAILURE;
                 goto out;
@@ -630,9 +638,11 @@ static void check_file(const config_t *cfg, worker_t *w, const char *filename, r
         rep_err(r, "[-] data file inconsistency: %d error(s)\n", errors);
     r->status = errors;
     if (cfg->trace)
-        fprintf(stderr, "[trace] %s: %zu B, engine %s, read %.2f ms, walk %.2f ms, checksum %.2f ms, format %.2f ms\n",
+        fprintf(stderr,
+                "[trace] %s: %zu B, engine %s, read %.2f ms, walk %.2f ms, checksum %.2f ms (of which waiting for the "
+                "GPU start-up %.2f ms), format %.2f ms\n",
                 filename, len, engine_used, (t_walk - t_read) * 1e3, (t_sum - t_walk) * 1e3, (t_fmt - t_sum) * 1e3,
-                (now_s() - t_fmt) * 1e3);
+                gpu_wait_ms, (now_s() - t_fmt) * 1e3);
 out:
     free(recs);
     free(offs);
@@ -788,6 +798,13 @@ int main(int argc, char *argv[]) {
     free(s.done);
     free(wa);
     free(th);
+    if (cfg.trace && cfg.engine != ENGINE_CPU) {
+        pthread_mutex_lock(&g_gpu_mu);
+        if (g_gpu_ok >= 0)
+            fprintf(stderr, "[trace] GPU start-up: library load + device count %.2f ms, first batch %.2f ms\n",
+                    (g_gpu_t_count - g_gpu_t0) * 1e3, (g_gpu_t_up - g_gpu_t_count) * 1e3);
+        pthread_mutex_unlock(&g_gpu_mu);
+    }
     if (cfg.engine != ENGINE_CPU) {
         /* the GPU start-up thread may still be inside the HIP runtime (auto
          * engine, nothing needed it): end without running teardown under it */
