@@ -689,9 +689,19 @@ def main():
     import torch.distributed as dist
     import zdbcrc
 
+    # one rank per GPU (the driver's N-GPU runs: RCCL for the barrier and the
+    # max-over-ranks time; the path itself exchanges nothing).  More ranks than
+    # GPUs -- a rehearsal of the N-rank plumbing on a one-GPU box -- share the
+    # devices round-robin and use gloo, which allows that.
+    ndev = torch.cuda.device_count()
+    local = local % max(ndev, 1)
     torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if world <= ndev:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            log(f"rank {rank}: {world} ranks on {ndev} GPU(s): gloo, device {local} shared")
+            dist.init_process_group("gloo")
 
     def barrier():
         if world > 1:
