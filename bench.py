@@ -595,6 +595,41 @@ def gather_ranks(obj, world: int) -> list:
     return out
 
 
+def read_ceiling(arena, nbytes: int, achieved_gbs: float):
+    """the achievable HBM read ceiling on THIS box, measured right
+    after the timed steps over the same 4 GiB arena -- read-only streaming
+    probes of the checksum kernel's access shape (each wave its own contiguous
+    slice, 1 KiB per load instruction, nontemporal loads; U = 4 or 8 loads in
+    flight per lane).  The probes live in the diagnostic library
+    (libzdbcrc_diag.so, never in the product library); None if it is absent."""
+    import ctypes
+    import torch
+    lib_path = ROOT / "0-db_amd" / "lib" / "libzdbcrc_diag.so"
+    if not lib_path.exists():
+        return None
+    lib = ctypes.CDLL(str(lib_path))
+    probe = lib.zdbcrc_debug_stream_read
+    probe.restype = ctypes.c_float
+    probe.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]
+    sink = torch.zeros(1 << 16, dtype=torch.int32, device="cuda")
+    st = torch.cuda.current_stream().cuda_stream
+    nb = nbytes // 16 * 16
+    best = None
+    runs = {}
+    for code, name in ((-104, "slices_nt_u4_wg1024"), (-204, "slices_nt_u4_wg768"), (-108, "slices_nt_u8_wg1024")):
+        ts = [probe(arena.data_ptr(), nb, sink.data_ptr(), code, st) for _ in range(7)][2:]
+        if min(ts) <= 0:
+            return None
+        tbs = nb / (float(np.median(ts)) / 1e3) / 1e12
+        runs[name] = round(tbs, 3)
+        if best is None or tbs > best[1]:
+            best = (name, tbs)
+    del sink
+    return {"probe": best[0], "tbs": round(best[1], 3), "frac_of_spec": round(best[1] * 1e3 / HBM_PEAK_GBS, 4),
+            "probes_tbs": runs, "bytes": nb,
+            "kernel_frac_of_ceiling": round(achieved_gbs / (best[1] * 1e3), 4)}
+
+
 def launch_ranks(args) -> int:
     """`python bench.py --gpus N` outside torch.distributed.run: start N rank
     processes (one per GPU) before this process touches any GPU, with the
@@ -773,6 +808,8 @@ def main():
                 "alg_bytes_per_launch": alg_bytes}
 
     extra = {}
+    if rank == 0 and world == 1 and not args.no_extra:
+        extra["read_ceiling"] = read_ceiling(arena, total, achieved)
     if not args.no_extra and not args.no_c4:
         del arena
         torch.cuda.empty_cache()
