@@ -655,6 +655,26 @@ def test_set_pipeline_gpu_engine_matches_reference_daemon(tmp_path, batch, datas
         assert without_clock(files[name]) == without_clock(ref_files[name]), name
 
 
+@pytest.mark.parametrize("engine", ["hip", "auto"])
+def test_set_pipeline_gpu_large_values(tmp_path, engine):
+    """values up to the 8 MiB maximum payload (data.h:6) through the GPU
+    engine, datafile rotation between them: the reference zdbd's replies and
+    datafiles"""
+    import json
+    from test_set_pipeline import ZDBD, build_stream_large, run_harness, run_reference_zdbd, without_clock
+    if not ZDBD.exists():
+        pytest.skip("oracle/_ref/zdbd not built")
+    stream, nreq = build_stream_large(9)
+    reps, ref_files = run_reference_zdbd(stream, nreq, tmp_path, 20 << 20)
+    out, files, stats = run_harness(stream, tmp_path, 20 << 20, engine, 16, from_file=True)
+    st = json.loads(stats.strip().splitlines()[-1])
+    assert st["engine"] == engine and st["gpu_batches"] > 0
+    assert out == b"".join(reps)
+    assert sorted(files) == sorted(ref_files) and len(files) > 1
+    for name in files:
+        assert without_clock(files[name]) == without_clock(ref_files[name]), name
+
+
 def test_set_pipeline_auto_engine_splits_batches(tmp_path):
     """--engine=auto: batches of at least 512 KiB of values on the GPU, the
     smaller ones on the scalar engine, replies and datafiles still those of

@@ -59,6 +59,26 @@ def build_stream(seed: int, n: int = 400):
     return b"".join(out), nreq
 
 
+def build_stream_large(seed: int, n: int = 24):
+    """pipelined SETs of large values up to the maximum payload
+    (ZDB_DATA_MAX_PAYLOAD, libzdb/data.h:6 = 8 MiB): overwrites, identical
+    re-SETs and small values in between"""
+    rng = np.random.default_rng(seed)
+    keys = [b"big-%d" % i for i in range(n // 3)]
+    last = {}
+    out = []
+    for i in range(n):
+        k = keys[int(rng.integers(len(keys)))]
+        if k in last and rng.random() < 0.2:
+            v = last[k]
+        else:
+            size = int(rng.choice([0, 100, 1 << 20, (3 << 20) + 7, 8 << 20]))
+            v = oracle.splitmix_bytes(size, seed * 1000 + i).tobytes()
+        last[k] = v
+        out.append(resp_set(k, v))
+    return b"".join(out), n
+
+
 def read_replies(data: bytes, count: int):
     """split RESP replies ($-1, $n + bulk, -error); None if incomplete"""
     out, p = [], 0
@@ -162,6 +182,18 @@ def test_set_pipeline_matches_reference_daemon(tmp_path, datasize, batch):
     for name in files:
         assert without_clock(files[name]) == without_clock(ref_files[name]), name
     assert b"$-1\r\n" in out and b"-Key too large\r\n" in out and b"-Invalid argument, key needed\r\n" in out
+
+
+@needs_ref
+def test_set_pipeline_large_values_match_reference_daemon(tmp_path):
+    """values up to the 8 MiB maximum, with datafile rotation between them"""
+    stream, nreq = build_stream_large(5)
+    reps, ref_files = run_reference_zdbd(stream, nreq, tmp_path, 20 << 20)
+    out, files, _ = run_harness(stream, tmp_path, 20 << 20, "cpu", 16)
+    assert out == b"".join(reps)
+    assert sorted(files) == sorted(ref_files) and len(files) > 1
+    for name in files:
+        assert without_clock(files[name]) == without_clock(ref_files[name]), name
 
 
 @needs_ref
