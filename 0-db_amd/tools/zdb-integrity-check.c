@@ -3,10 +3,11 @@
  *
  * Same command line, stdout, stderr and exit status as the reference tool
  * (tools/integrity-check/integrity-check.c:30-166) for one datafile, but
- * restructured for the MI355X: the datafile is read into pinned memory with
- * large reads, the host walks the entry headers (zdb_datafile_walk), every
- * payload checksum is computed in ONE batched GPU call (zdb_crc32_batch ->
- * crc32_hip.hip), and the report is formatted in a single buffer.  The
+ * restructured for the MI355X: the datafile is read with large reads and
+ * streamed into a device image, the host walks the entry headers
+ * (zdb_datafile_walk), every payload checksum is computed in ONE batched GPU
+ * pass over the image (crc32_hip.hip), and the report is formatted in a
+ * single buffer.  The
  * reference does 4 syscalls and ~7 printf per record around one CPU crc each
  * (integrity-check.c:59-105).
  *
@@ -18,10 +19,13 @@
  *        says so and exits 1 -- it never falls back silently;
  *   cpu  the scalar drop-in engine (zdb_crc32, crc32_cpu.c), e.g. to time the
  *        reference-compatible CPU path;
- *   auto the GPU for every file read after the GPU runtime is up, the scalar
- *        engine before (HIP start-up costs ~0.2 s, longer than reading and
- *        checking one 256 MiB datafile on a core: DESIGN.md §7).  Both
- *        engines are bit-exact, so the report does not depend on the choice.
+ *   auto the scalar engine when the whole scan would finish on the workers'
+ *        cores before the GPU could pay for its start-up (HIP start-up costs
+ *        ~0.2 s, longer than reading and checking one 256 MiB datafile on a
+ *        core: DESIGN.md §7; AUTO_* below); otherwise the GPU is started and
+ *        takes every file read after it is up, the scalar engine the files
+ *        before.  Both engines are bit-exact, so the report does not depend
+ *        on the choice.
  *
  * Ingest: the GPU runtime is brought up on a thread of its
  * own at start, while the workers read.  Each worker reads its file in 32 MiB
@@ -255,6 +259,15 @@ static double g_gpu_t0, g_gpu_t_count, g_gpu_t_up; /* start-up thread timeline (
 #define ENGINE_CPU 0
 #define ENGINE_HIP 1
 #define ENGINE_AUTO 2
+
+/* --engine=auto: bring the GPU up only when the scan can gain from it.  A
+ * worker checksums host memory at AUTO_CPU_GIBS on the scalar engine; the GPU
+ * engine pays AUTO_GPU_START_S of runtime start-up and moves the bytes over
+ * PCIe at AUTO_PCIE_GIBS (DESIGN.md §7.1 measures all three), so the GPU is
+ * started only when bytes / (workers * cpu) > start + bytes / pcie. */
+#define AUTO_CPU_GIBS 10.0
+#define AUTO_GPU_START_S 0.25
+#define AUTO_PCIE_GIBS 40.0
 
 #define READ_CHUNK (32u << 20)  /* pread size: one H2D chunk per read */
 #define SLOT_BYTES (8u << 20)   /* pinned staging slot */
@@ -730,9 +743,27 @@ int main(int argc, char *argv[]) {
         cfg.stale_errno = errno;
     }
 
+    int njobs = jobs > 0 ? jobs : (argc - argi < 8 ? argc - argi : 8);
+    if (njobs > argc - argi)
+        njobs = argc - argi;
+    const char *force_gpu = getenv("ZDBCRC_AUTO_START_GPU"); /* tests: start the GPU whatever the size */
+    if (cfg.engine == ENGINE_AUTO && !(force_gpu && force_gpu[0] == '1')) {
+        double gib = 0;
+        for (int i = argi; i < argc; i++) {
+            struct stat fst;
+            if (stat(argv[i], &fst) == 0)
+                gib += (double)fst.st_size / (double)(1u << 30);
+        }
+        if (gib / (njobs * AUTO_CPU_GIBS) <= AUTO_GPU_START_S + gib / AUTO_PCIE_GIBS)
+            g_gpu_ok = 0; /* the scalar engine finishes first: no GPU start-up */
+        if (cfg.trace)
+            fprintf(stderr, "[trace] auto engine: %.2f GiB over %d worker(s): %s\n", gib, njobs,
+                    g_gpu_ok == 0 ? "scalar engine (the GPU start-up would not pay)" : "GPU once it is up");
+    }
+
     /* GPU start-up overlaps the reads (the thread is never joined: a
      * worker that needs the GPU waits for it; exit does not) */
-    if (cfg.engine != ENGINE_CPU) {
+    if (cfg.engine == ENGINE_HIP || (cfg.engine == ENGINE_AUTO && g_gpu_ok != 0)) {
         pthread_t gt;
         if (pthread_create(&gt, NULL, gpu_init_main, &cfg.gpus) != 0)
             g_gpu_ok = 0;
@@ -800,7 +831,7 @@ int main(int argc, char *argv[]) {
     free(th);
     if (cfg.trace && cfg.engine != ENGINE_CPU) {
         pthread_mutex_lock(&g_gpu_mu);
-        if (g_gpu_ok >= 0)
+        if (g_gpu_ok >= 0 && g_gpu_t0 > 0)
             fprintf(stderr, "[trace] GPU start-up: library load + device count %.2f ms, first batch %.2f ms\n",
                     (g_gpu_t_count - g_gpu_t0) * 1e3, (g_gpu_t_up - g_gpu_t_count) * 1e3);
         pthread_mutex_unlock(&g_gpu_mu);

@@ -325,8 +325,9 @@ TOOL_CASES = ["mixed", "zipf_small", "fixed_4k", "corrupt_payload", "corrupt_crc
 
 @pytest.mark.parametrize("engine", ["hip", "auto"])
 @pytest.mark.parametrize("name", TOOL_CASES)
-def test_tool_gpu_engine_matches_reference(tmp_path, datafile_cases, name, engine):
+def test_tool_gpu_engine_matches_reference(tmp_path, datafile_cases, name, engine, monkeypatch):
     from test_tool_cpu import expected, run_tool
+    monkeypatch.setenv("ZDBCRC_AUTO_START_GPU", "1")  # auto: start the GPU even for a small scan
     out, err, code = run_tool(name, tmp_path, engine)
     eout, eerr = expected(name)
     assert out == eout
@@ -360,7 +361,8 @@ def big_datafile(tmp_path_factory):
 @pytest.mark.parametrize("engine", ["hip", "auto"])
 def test_tool_gpu_256MiB_matches_reference(big_datafile, engine):
     """the GPU tool on a reference-written 256 MiB datafile (three corrupt
-    payloads): stdout, stderr and exit status of the reference tool"""
+    payloads): stdout, stderr and exit status of the reference tool (auto: with
+    its own start-up policy, i.e. the scalar engine for one 256 MiB file)"""
     import re
     path, ref = big_datafile
     from test_tool_cpu import TOOL
@@ -409,12 +411,12 @@ def large_value_datafile(request, tmp_path_factory):
 @pytest.mark.parametrize("engine", ["hip", "auto"])
 def test_tool_gpu_large_values_match_reference(large_value_datafile, engine):
     """the GPU tool on 8 MiB (maximum) and Zipf-mixed values: the reference
-    tool's stdout, stderr and exit status"""
+    tool's stdout, stderr and exit status (auto: GPU start forced)"""
     import re
     path, ref = large_value_datafile
     from test_tool_cpu import TOOL
     p = subprocess.run([str(TOOL), f"--engine={engine}", str(path)], capture_output=True,
-                       env=dict(os.environ, TZ="UTC"), timeout=120)
+                       env=dict(os.environ, TZ="UTC", ZDBCRC_AUTO_START_GPU="1"), timeout=120)
     t = re.compile(rb"\[\s*\d+\.\d{6}\]")
     assert p.returncode == ref.returncode
     assert t.sub(b"[T]", p.stdout) == t.sub(b"[T]", ref.stdout)

@@ -135,3 +135,28 @@ def test_worker_to_device_mapping(tmp_path, datafile_cases, jobs, gpus, devices)
 def test_bad_option_is_usage_error(tmp_path):
     p = subprocess.run([str(TOOL), "--jobs=0", str(tmp_path / "zdb-data-0")], capture_output=True)
     assert p.returncode == 1 and b"Usage:" in p.stderr
+
+
+def test_auto_engine_start_up_policy(tmp_path, datafile_cases):
+    """--engine=auto starts the GPU only when the scan cannot finish on the
+    workers' cores before the GPU start-up would pay for itself: a small scan
+    never starts it (ZDBCRC_AUTO_START_GPU=1 forces the start, for tests)"""
+    import os
+    import shutil
+    import subprocess
+    from test_tool_cpu import GOLDEN, TOOL
+    d = tmp_path / "m"
+    d.mkdir()
+    shutil.copy(GOLDEN / "datafiles" / "mixed.d0", d / "d0")
+    os.symlink("d0", d / "zdb-data-0")
+    base = dict(os.environ, TZ="UTC", ZDBCRC_TOOL_TRACE="1")
+    base.pop("ZDBCRC_AUTO_START_GPU", None)
+    p = subprocess.run([str(TOOL), "--engine=auto", str(d / "zdb-data-0")], capture_output=True, env=base,
+                       timeout=60)
+    assert b"auto engine:" in p.stderr and b"scalar engine (the GPU start-up would not pay)" in p.stderr
+    assert b"GPU start-up:" not in p.stderr
+    p = subprocess.run([str(TOOL), "--engine=auto", str(d / "zdb-data-0")], capture_output=True,
+                       env=dict(base, ZDBCRC_AUTO_START_GPU="1"), timeout=60)
+    assert b"auto engine:" not in p.stderr  # no policy: the start-up thread runs
+    assert p.returncode == {c["name"]: c for c in datafile_cases}["mixed"]["exit"]
+
