@@ -15,11 +15,11 @@
  *                              <dir>/zdb-data-<id> [<dir>/zdb-data-<id> ...]
  *
  * Engines:
- *   hip  (default) every checksum on the GPU; if the GPU cannot run, the tool
- *        says so and exits 1 -- it never falls back silently;
+ *   hip  every checksum on the GPU; if the GPU cannot run, the tool says so
+ *        and exits 1 -- it never falls back silently;
  *   cpu  the scalar drop-in engine (zdb_crc32, crc32_cpu.c), e.g. to time the
  *        reference-compatible CPU path;
- *   auto the scalar engine when the whole scan would finish on the workers'
+ *   auto (default) the scalar engine when the whole scan would finish on the workers'
  *        cores before the GPU could pay for its start-up (HIP start-up costs
  *        ~0.2 s, longer than reading and checking one 256 MiB datafile on a
  *        core: DESIGN.md §7; AUTO_* below); otherwise the GPU is started and
@@ -712,7 +712,7 @@ static void usage(const char *prog) {
 }
 
 int main(int argc, char *argv[]) {
-    config_t cfg = {ENGINE_HIP, 0, 0, getenv("ZDBCRC_TOOL_TRACE") != NULL};
+    config_t cfg = {ENGINE_AUTO, 0, 0, getenv("ZDBCRC_TOOL_TRACE") != NULL};
     int jobs = 0;
     int argi = 1;
     while (argi < argc && strncmp(argv[argi], "--", 2) == 0) {

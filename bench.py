@@ -470,7 +470,7 @@ def e2e_legs(offs, lens, seed) -> dict:
         with open(f"{td}/d0", "wb") as f:
             f.write(zdbcrc.encode_header(0) + body)
         os.symlink("d0", f"{td}/zdb-data-0")
-        tools = {"gpu_tool": [str(ROOT / "0-db_amd/bin/zdb-integrity-check"), f"{td}/zdb-data-0"],
+        tools = {"gpu_tool": [str(ROOT / "0-db_amd/bin/zdb-integrity-check"), "--engine=hip", f"{td}/zdb-data-0"],
                  "auto_engine_tool": [str(ROOT / "0-db_amd/bin/zdb-integrity-check"), "--engine=auto",
                                       f"{td}/zdb-data-0"],
                  "scalar_engine_tool": [str(ROOT / "0-db_amd/bin/zdb-integrity-check"), "--engine=cpu",
@@ -500,10 +500,10 @@ def e2e_legs(offs, lens, seed) -> dict:
         tool = str(ROOT / "0-db_amd/bin/zdb-integrity-check")
         scan = {"files": len(files), "file_bytes": 28 + len(body)}
         files32 = files * 4  # 32 files: a store large enough for the GPU start-up to pay off
-        runs = {"gpu_tool_jobs8": ([[tool, "--jobs=8"] + files], 8),
+        runs = {"gpu_tool_jobs8": ([[tool, "--engine=hip", "--jobs=8"] + files], 8),
                 "auto_engine_tool_jobs8": ([[tool, "--engine=auto", "--jobs=8"] + files], 8),
                 "scalar_engine_tool_jobs8": ([[tool, "--engine=cpu", "--jobs=8"] + files], 8),
-                "gpu_tool_jobs8_32files": ([[tool, "--jobs=8"] + files32], 32),
+                "gpu_tool_jobs8_32files": ([[tool, "--engine=hip", "--jobs=8"] + files32], 32),
                 "auto_engine_tool_jobs8_32files": ([[tool, "--engine=auto", "--jobs=8"] + files32], 32),
                 "scalar_engine_tool_jobs8_32files": ([[tool, "--engine=cpu", "--jobs=8"] + files32], 32)}
         if oracle.REF_INTEGRITY.exists():
@@ -519,7 +519,7 @@ def e2e_legs(offs, lens, seed) -> dict:
             scan[name + "_s"] = round(min(ts), 4)
             scan[name + "_gibs"] = round(nf * (28 + len(body)) / min(ts) / GIB, 2)
         # where the time goes in one GPU-engine run (ZDBCRC_TOOL_TRACE)
-        p = subprocess.run([tool, "--jobs=8"] + files, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE,
+        p = subprocess.run([tool, "--engine=hip", "--jobs=8"] + files, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE,
                            env=dict(os.environ, ZDBCRC_TOOL_TRACE="1"), timeout=300)
         scan["gpu_tool_trace"] = [ln for ln in p.stderr.decode().splitlines() if ln.startswith("[trace]")][:8]
         res["integrity_scan_8x256MiB"] = scan

@@ -62,3 +62,23 @@ def test_tool_argument_errors(tmp_path):
     assert p.returncode == 1
     assert b"d5: No such file or directory" in p.stderr
     assert p.stderr.endswith(b"[-] data file inconsistency: 1 error(s)\n")
+
+
+def test_default_engine_is_auto(tmp_path, datafile_cases):
+    """No --engine: the auto engine, which checks a small store on the scalar
+    engine without starting the GPU runtime -- so the reference's command line
+    gives the reference's report here too (this container has no GPU: the hip
+    engine would exit 1 with "GPU engine unavailable")."""
+    d = tmp_path / "mixed"
+    d.mkdir()
+    shutil.copy(GOLDEN / "datafiles" / "mixed.d0", d / "d0")
+    os.symlink("d0", d / "zdb-data-0")
+    p = subprocess.run([str(TOOL), str(d / "zdb-data-0")], capture_output=True, timeout=120,
+                       env=dict(os.environ, TZ="UTC", ZDBCRC_TOOL_TRACE="1"))
+    norm = lambda s: TIMELOG.sub("[T]", s.decode().replace(str(d), "@DIR@"))
+    eout, eerr = expected("mixed")
+    assert norm(p.stdout) == eout
+    err = "".join(ln + "\n" for ln in norm(p.stderr).splitlines() if not ln.startswith("[trace]"))
+    assert err == eerr
+    assert p.returncode == {c["name"]: c for c in datafile_cases}["mixed"]["exit"]
+    assert "auto engine" in p.stderr.decode() and "engine cpu" in p.stderr.decode()
