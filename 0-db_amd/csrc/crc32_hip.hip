@@ -83,6 +83,13 @@ constexpr uint64_t DYN_MIN_UNITS_PER_WAVE = 4096;
 constexpr uint64_t DYN_MAX_CHUNKS_PER_RECORD = 64;
 // records up to this many bytes take the small-record loop shape (PP)
 constexpr uint64_t SMALL_RECORD_MAX = 4096;
+// record-relative grids of records this long load from the dword below the
+// record and fold its last bytes in at the end (next_seg_batched): the fold
+// waits for one dword load at the record's end, which small records cannot
+// pay for (C2u: 4 KiB values behind 26-byte headers, +8 %) and large ones
+// recoup many times over (C3: the 1 MiB values, a third of the bytes, -2.7 %;
+// profiles/r2/ab_dword_grid*.jsonl)
+constexpr uint64_t DWG_MIN_BYTES = 64 * 1024;
 
 static_assert(ZDBCRC_LDS_DW % 4 == 0, "LDS image must be 16-byte granular");
 static_assert(ZDBCRC_LDS_DW * 4 * WG_PER_CU <= 160 * 1024, "LDS budget");
@@ -422,7 +429,7 @@ __device__ __forceinline__ void load_meta(MetaBatch &m, uint64_t rb, uint64_t n,
     }
 }
 
-template <uint32_t UO>
+template <uint32_t UO, bool BMG = false>
 __device__ __forceinline__ bool next_seg_batched(uint64_t &r, uint64_t n, uint64_t ub, uint64_t ue, uint32_t lane,
                                                  MetaBatch &m, const UnitPrefix &unit_start,
                                                  const uint8_t *arena, const uint64_t *__restrict__ offsets,
@@ -448,12 +455,20 @@ __device__ __forceinline__ bool next_seg_batched(uint64_t &r, uint64_t n, uint64
             sg.us = us;
             sg.c.np = (uint32_t)(ur - us);
             // record-relative grid iff the planner counted fewer pieces than
-            // the aligned grid has (record_pieces)
+            // the aligned grid has (record_pieces).  For records of at least
+            // DWG_MIN_BYTES its loads start at the dword below the record
+            // (byte-misaligned 16-byte loads stream ~20 % slower than
+            // dword-aligned ones, misalign_probe.jsonl): the h = A mod 4 bytes
+            // before the record are masked off and the record's last h bytes,
+            // which the grid then misses, are folded in at its end
+            // (seg_value_v3, z = 16 + h); aligned grid: z = the trailing pad of
+            // the last piece.  BMG (A/B only): byte-misaligned loads for all
             const bool rel = sg.c.np != (uint32_t)pieces_aligned(A, Aend - A);
-            sg.c.P0 = rel ? A : (A & ~15ull);
-            sg.z = (uint32_t)(sg.c.P0 + 16u * (uint64_t)sg.c.np - Aend);
-            sg.c.lo0 = rel ? 0 : (int)(A & 15u);
-            sg.c.hi_last = 16 - (int)sg.z;
+            const uint32_t h = rel && !BMG && Aend - A >= DWG_MIN_BYTES ? (uint32_t)(A & 3u) : 0u;
+            sg.c.P0 = rel ? A - h : (A & ~15ull);
+            sg.z = rel ? (h ? 16u + h : 0u) : (uint32_t)(sg.c.P0 + 16u * (uint64_t)sg.c.np - Aend);
+            sg.c.lo0 = rel ? (int)h : (int)(A & 15u);
+            sg.c.hi_last = rel ? 16 : 16 - (int)sg.z;
             sg.c.pa = (uint32_t)(s_lo - us);
             sg.pb = (uint32_t)(s_hi - us);
             const uint32_t T = (sg.pb - sg.c.pa + 63u) / 64u;
@@ -491,8 +506,18 @@ __device__ __forceinline__ void load_superstep_v3(const SegCtx &s, uint32_t ss, 
 template <int NOZ = 0>
 __device__ __forceinline__ uint32_t seg_value_v3(const Seg &sg, uint32_t acc, uint32_t lane, const uint32_t *lds,
                                                  const uint32_t *__restrict__ tables) {
+    // record-relative grid from the dword below the record (z = 16 + h): the
+    // segment that ends the record folds in its last h bytes y (one aligned
+    // dword, loaded before the reduction so that its latency hides behind it),
+    // crc(X || y) = shift(crc(X) ^ y, h); the other segments only shift by h
+    const bool fold = sg.z >= 16u;
+    uint32_t y = 0;
+    if (fold && sg.pb == sg.c.np)
+        y = *reinterpret_cast<const uint32_t *>(sg.c.P0 + 16u * (uint64_t)sg.c.np) & ((1u << (8u * (sg.z - 16u))) - 1u);
     uint32_t x = wave_xor_scalar(NOZ >= 2 ? acc : lane_place(acc, lane, lds));
-    if (!NOZ && sg.z)
+    if (fold)
+        x = uniform_shift(x ^ y, tables + ZDBCRC_OFF_F + (sg.z - 16u) * SCH * 32);
+    else if (!NOZ && sg.z)
         x = uniform_shift(x, tables + ZDBCRC_OFF_Z + sg.z * SCH * 32);
     // shift over the record pieces after the segment: one round per nonzero
     // radix-256 digit (at most 4 dependent table reads, usually 0-2)
@@ -565,7 +590,7 @@ __device__ __forceinline__ uint64_t block_excl_scan64(uint64_t v, uint64_t *wsum
 // are flushed with atomic XOR at each claim (at most 2 are pending then).
 template <int WGT, int WPE, bool STAMP = false, int PRIO = 0, uint32_t UO = UNIT_OVH, int NOZ = 0,
           bool NTL = false, bool NOLOAD = false, int XM = 0, int DYN = 0, int CPW = 4, uint32_t DYN_POOLS = 8,
-          bool SP = false, int PP = 0, bool SEGDUMP = false>
+          bool SP = false, int PP = 0, bool SEGDUMP = false, bool BMG = false>
 __global__ __launch_bounds__(WGT, WPE) void crc_batch_kernel_v3(
     const uint8_t *__restrict__ arena, const uint64_t *__restrict__ offsets,
     const uint32_t *__restrict__ lengths, const PlanArgs plan, uint64_t n,
@@ -651,7 +676,7 @@ __global__ __launch_bounds__(WGT, WPE) void crc_batch_kernel_v3(
     if (active) {
         rn = find_record(unit_start, n, ub, lane);
         load_meta(m, rn, n, lane, unit_start, arena, offsets, lengths);
-        active = next_seg_batched<UO>(rn, n, ub, ue, lane, m, unit_start, arena, offsets, lengths, cur);
+        active = next_seg_batched<UO, BMG>(rn, n, ub, ue, lane, m, unit_start, arena, offsets, lengths, cur);
         if (active)
             load_superstep_v3<NTL, NOLOAD>(cur.c, 0, lane, bufc);
     }
@@ -716,7 +741,7 @@ __global__ __launch_bounds__(WGT, WPE) void crc_batch_kernel_v3(
             rn = find_record(unit_start, n, ub, lane);
             if (rn < m.rb)
                 load_meta(m, rn, n, lane, unit_start, arena, offsets, lengths);
-            if (next_seg_batched<UO>(rn, n, ub, ue, lane, m, unit_start, arena, offsets, lengths, sg))
+            if (next_seg_batched<UO, BMG>(rn, n, ub, ue, lane, m, unit_start, arena, offsets, lengths, sg))
                 return true;
         }
     };
@@ -777,7 +802,7 @@ __global__ __launch_bounds__(WGT, WPE) void crc_batch_kernel_v3(
         if (css + 1 < cur.S) {                                                                                \
             nx = cur;                                                                                         \
             nss = css + 1;                                                                                    \
-        } else if (!next_seg_batched<UO>(rn, n, ub, ue, lane, m, unit_start, arena, offsets, lengths, nx) &&  \
+        } else if (!next_seg_batched<UO, BMG>(rn, n, ub, ue, lane, m, unit_start, arena, offsets, lengths, nx) &&  \
                    !(DYN && dyn && claim(nx))) {                                                              \
             more = false;                                                                                     \
             nx = cur;                                                                                         \
@@ -925,6 +950,10 @@ const KernelVariant kVariants[] = {
     {"v3_wg768_nt_dyn4c4p32_sp_noz_noplace", crc_batch_kernel_v3<768, 6, false, 0, UNIT_OVH, 2, true, false, 0, 4, 4, 32, true>, 768},
     // debugging: the default kernel writing each wave's last segment (pa, pb, value, r | np << 32)
     {"v3_wg768_nt_dyn4c4p32_sp_segdump", crc_batch_kernel_v3<768, 6, false, 0, UNIT_OVH, false, true, false, 0, 4, 4, 32, true, 0, true>, 768},
+    // round 2: the record-relative grid on byte-misaligned loads (BMG, the previous default) against the
+    // default's loads from the dword below the record
+    {"v3_wg768_nt_dyn4c4p32_sp_bmg", crc_batch_kernel_v3<768, 6, false, 0, UNIT_OVH, false, true, false, 0, 4, 4, 32, true, 0, false, true>, 768},
+    {"v3_wg768_nt_dyn4c4p32_sp_pp_wait_bmg", crc_batch_kernel_v3<768, 6, false, 0, UNIT_OVH, false, true, false, 0, 4, 4, 32, true, 3, false, true>, 768},
 };
 constexpr int kNumVariants = (int)(sizeof(kVariants) / sizeof(kVariants[0]));
 std::atomic<int> g_variant{-1};
@@ -956,8 +985,11 @@ const KernelVariant &variant(bool /*small: the A/B harness picks by index*/ = fa
 const KernelVariant kDefault = {"v3_wg768_nt_dyn4c4p32_sp",
                                 crc_batch_kernel_v3<768, 6, false, 0, UNIT_OVH, false, true, false, 0, 4, 4, 32, true>,
                                 768};
-const KernelVariant kSmall = {"v3_wg768_nt_dyn4c4p32_sp_pp_wait",
-                              crc_batch_kernel_v3<768, 6, false, 0, UNIT_OVH, false, true, false, 0, 4, 4, 32, true, 3>,
+// (its records are below DWG_MIN_BYTES, so it is built without the dword
+// grid's code: BMG)
+const KernelVariant kSmall = {"v3_wg768_nt_dyn4c4p32_sp_pp_wait_bmg",
+                              crc_batch_kernel_v3<768, 6, false, 0, UNIT_OVH, false, true, false, 0, 4, 4, 32, true, 3,
+                                                  false, true>,
                               768};
 const KernelVariant &variant(bool small = false) { return small ? kSmall : kDefault; }
 #endif

@@ -189,4 +189,13 @@ void zdbcrc_build_tables(uint32_t *img) {
                 fill_linear(img + ZDBCRC_OFF_R + ((j * 256 + d) * ZDBCRC_SCH + c) * 32, 1, b);
             }
         }
+
+    for (int h = 0; h < 4; h++) {
+        const uint32_t m = xpow(8 * (uint64_t)h, 0);
+        for (int c = 0; c < ZDBCRC_SCH; c++) {
+            for (int t = 0; t < 5; t++)
+                b[t] = multmodp(m, reg_slice(1u << t, c));
+            fill_linear(img + ZDBCRC_OFF_F + (h * ZDBCRC_SCH + c) * 32, 1, b);
+        }
+    }
 }

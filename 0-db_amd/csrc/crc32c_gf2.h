@@ -51,7 +51,8 @@ uint32_t zdbcrc_update_bytes(uint32_t crc, const uint8_t *p, size_t n);
 #define ZDBCRC_LDS_DW   (ZDBCRC_OFF_L + ZDBCRC_SCH * 32 * ZDBCRC_WAVE) /* end of LDS image  */
 #define ZDBCRC_OFF_Z    ZDBCRC_LDS_DW                                  /* [16][SCH][32]     */
 #define ZDBCRC_OFF_R    (ZDBCRC_OFF_Z + 16 * ZDBCRC_SCH * 32)          /* [RDIG][256][SCH][32] */
-#define ZDBCRC_TABLE_DW (ZDBCRC_OFF_R + ZDBCRC_RDIG * 256 * ZDBCRC_SCH * 32)
+#define ZDBCRC_OFF_F    (ZDBCRC_OFF_R + ZDBCRC_RDIG * 256 * ZDBCRC_SCH * 32) /* [4][SCH][32] */
+#define ZDBCRC_TABLE_DW (ZDBCRC_OFF_F + 4 * ZDBCRC_SCH * 32)
 
 /*
  * Piece windows.  A 16-byte piece (dwords w0..w3, little endian) is covered
@@ -81,6 +82,9 @@ int zdbcrc_window_bit(int j, int t);
  * Z[z][c][v] : shift(v << 5c, -z), z = 0..15   (trailing pad removal)
  * R[j][d][c][v] : shift(v << 5c, 16 * d * 256^j) (shift by a piece count,
  *              one radix-256 digit per table: at most 4 dependent rounds)
+ * F[h][c][v] : shift(v << 5c, h), h = 0..3     (a record-relative grid loaded
+ *              from the dword below the record: its last h bytes y are folded
+ *              in at the end as crc(X || y) = shift(crc(X) ^ y, h))
  */
 void zdbcrc_build_tables(uint32_t *image /* ZDBCRC_TABLE_DW dwords */);
 

@@ -68,11 +68,18 @@ constexpr uint32_t WALK_T = 256;
 // search: threads per chunk, KiB per wave block; each lane loads its own 16
 // bytes only and takes the next 16 from its neighbour (walk 0.58 -> 0.51 ms
 // on C4, profiles/r2/walk_search_ab*.jsonl)
-constexpr int SEARCH_T = 256, SEARCH_SU = 8;
+// at most 80 VGPRs (6 waves per SIMD instead of 5 at the compiler's 82:
+// walk 0.502 -> 0.480 ms with the windowed chain below, profiles/r2/
+// walk_occupancy_window_chain_ab.jsonl; 64 VGPRs spill, 4 KiB blocks are slower)
+constexpr int SEARCH_T = 256, SEARCH_SU = 8, SEARCH_MW = 6;
 // chains per wave (A2, C2): the lanes of a wave hop in lockstep, each hop
 // waiting for the slowest of its lanes' header loads, so fewer chains per
 // wave on more CUs shorten every hop
 constexpr uint32_t CHAINS_PER_WAVE = 16;
+// A2 shape: one wave per chunk reading 1 KiB windows (walk_spec_win_kernel)
+// instead of one lane per chunk reading each header (C4: walk -1.5 to -3 %
+// in two A/B rounds, the same records and exits: GPU walk tests)
+constexpr bool WINDOW_CHAIN = true;
 
 // little-endian u32 at any byte address: two aligned dword loads + one
 // v_alignbyte (reads up to 7 bytes past p; images are readable 16 bytes past
@@ -355,8 +362,8 @@ __device__ __forceinline__ uint64_t scan_block(const uint8_t *f, uint64_t len, u
 // not (most bytes are in the large values), uniformly within it, so the
 // nearer of the two ends is found in half the scanning on average and in
 // the worst case.
-template <int NT, int SU, bool NOA1 = false>
-__global__ __launch_bounds__(NT) void walk_search_kernel(FileTab t, uint64_t *__restrict__ s_start,
+template <int NT, int SU, bool NOA1 = false, int MW = 1>
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MW))) void walk_search_kernel(FileTab t, uint64_t *__restrict__ s_start,
                                                          int32_t *__restrict__ s_status) {
     constexpr uint32_t NWS = NT / 64, NF = NWS / 2, NB = NWS - NF;
     constexpr uint64_t SB = 1024u * SU; // bytes per wave block
@@ -470,6 +477,129 @@ __global__ __launch_bounds__(64) void walk_spec_kernel(FileTab t, const uint64_t
     s_exit[w] = exit;
     s_count[w] = count;
     s_status[w] = st;
+}
+
+// A2 with a 1 KiB window per round trip (one wave per chunk): lane l holds
+// bytes [16 l, 16 l + 16) of the window that starts at the 16-byte block of
+// the current header, so every header that lies inside the window (C3 sizes:
+// the records of the small buckets, 64 B - 1 KiB, two thirds of all records)
+// is decoded from registers (readlane) instead of a dependent HBM round trip.
+// Same records, exits and terminal states as walk_chain<SPEC> -- the bytes
+// are the same, only fetched in larger pieces: a header whose 13 decoded
+// bytes [pos, pos + 13) reach past the window is fetched by a new window at
+// pos; lanes whose 16-byte block starts past the file's end load nothing
+// (the image is readable 16 bytes past a file's end, not more), and such
+// bytes only matter for a header that cannot fit (SHORT_HEADER either way).
+struct Window {
+    uint4 v;        // this lane's 16 bytes
+    uintptr_t base; // image address of lane 0's block (16-aligned), uniform
+};
+
+__device__ __forceinline__ void load_window(Window &w, const uint8_t *f, uint64_t len, uint64_t pos, uint32_t lane) {
+    w.base = reinterpret_cast<uintptr_t>(f + pos) & ~uintptr_t(15);
+    const uintptr_t a = w.base + 16u * lane;
+    const uintptr_t end = reinterpret_cast<uintptr_t>(f + len);
+    w.v = make_uint4(0, 0, 0, 0);
+    if (a <= end) {
+        typedef const __attribute__((address_space(1))) uint32_t gx4 __attribute__((ext_vector_type(4)));
+        const auto x = *reinterpret_cast<gx4 *>(a);
+        w.v = make_uint4(x.x, x.y, x.z, x.w);
+    }
+}
+
+// the header fields at window byte offset off (uniform, off + 13 <= 1024)
+__device__ __forceinline__ Hdr window_hdr(const Window &w, uint32_t off) {
+    const uint32_t a = off >> 4, b = a < 63 ? a + 1 : a;
+    uint32_t d[8] = {(uint32_t)__builtin_amdgcn_readlane(w.v.x, a), (uint32_t)__builtin_amdgcn_readlane(w.v.y, a),
+                     (uint32_t)__builtin_amdgcn_readlane(w.v.z, a), (uint32_t)__builtin_amdgcn_readlane(w.v.w, a),
+                     (uint32_t)__builtin_amdgcn_readlane(w.v.x, b), (uint32_t)__builtin_amdgcn_readlane(w.v.y, b),
+                     (uint32_t)__builtin_amdgcn_readlane(w.v.z, b), (uint32_t)__builtin_amdgcn_readlane(w.v.w, b)};
+    const uint32_t k = (off & 15u) >> 2, sh = 8u * (off & 3u);
+    if (k & 2u) {
+#pragma unroll
+        for (int i = 0; i < 6; i++)
+            d[i] = d[i + 2];
+    }
+    if (k & 1u) {
+#pragma unroll
+        for (int i = 0; i < 5; i++)
+            d[i] = d[i + 1];
+    }
+    uint32_t q[4];
+#pragma unroll
+    for (int i = 0; i < 4; i++)
+        q[i] = (uint32_t)((((uint64_t)d[i + 1] << 32) | d[i]) >> sh);
+    return Hdr{q[0] & 0xFFu, (q[0] >> 8) | (q[1] << 24), (q[2] >> 8) | (q[3] << 24)};
+}
+
+__device__ __forceinline__ bool in_window(const Window &w, const uint8_t *f, uint64_t pos) {
+    return reinterpret_cast<uintptr_t>(f + pos) - w.base + 13u <= 1024u;
+}
+
+__global__ __launch_bounds__(64) void walk_spec_win_kernel(FileTab t, const uint64_t *__restrict__ s_start,
+                                                           uint64_t *__restrict__ s_exit,
+                                                           uint32_t *__restrict__ s_count,
+                                                           int32_t *__restrict__ s_status, RecSlot *__restrict__ slots,
+                                                           uint32_t kcap) {
+    const uint64_t w = blockIdx.x;
+    const uint32_t lane = threadIdx.x;
+    const uint64_t start = s_start[w];
+    if (start == NONE)
+        return;
+    const uint32_t fi = (uint32_t)(w / t.cpf), c = (uint32_t)(w % t.cpf);
+    const uint64_t len = t.file_len[fi];
+    const uint8_t *f = t.image + t.file_off[fi];
+    const uint64_t cend = ((uint64_t)c + 1) << t.lg;
+    RecSlot *sl = slots + w * kcap;
+    uint32_t count = 0;
+    int32_t st = ST_CONTINUE;
+    uint64_t pos = start;
+    Window win;
+    if (pos < cend && pos < len)
+        load_window(win, f, len, pos, lane);
+    while (pos < cend) {
+        if (pos >= len) { // clean end of file (pos == len)
+            st = ZDB_WALK_OK;
+            break;
+        }
+        const Hdr h = window_hdr(win, (uint32_t)(reinterpret_cast<uintptr_t>(f + pos) - win.base));
+        const uint32_t hlen = ZDB_ENTRY_HEADER_SIZE + h.idl;
+        if (pos + hlen > len) {
+            st = ZDB_WALK_SHORT_HEADER;
+            break;
+        }
+        const uint32_t L = h.L;
+        uint64_t next = pos + hlen;
+        int32_t s = ST_CONTINUE;
+        if (L) {
+            if (next + L > len)
+                s = ZDB_WALK_SHORT_PAYLOAD;
+            else
+                next += L;
+        }
+        // the next header's window, when it is not this one (issued before the
+        // slot store: the memory counter completes in order)
+        if (s == ST_CONTINUE && next < len && next < cend && !in_window(win, f, next))
+            load_window(win, f, len, next, lane);
+        __asm__ volatile("" ::: "memory");
+        if (count < kcap && lane == 0) {
+            const bool full = s == ST_CONTINUE && L > 0;
+            sl[count] = RecSlot{(uint32_t)pos, full ? L : 0u, full ? h.integ : 0u, hlen};
+        }
+        count++;
+        if (s == ZDB_WALK_SHORT_PAYLOAD) {
+            st = s;
+            break;
+        }
+        pos = next;
+    }
+    if (st == ST_CONTINUE && pos >= len)
+        st = ZDB_WALK_OK;
+    if (lane == 0) {
+        s_exit[w] = pos;
+        s_count[w] = count;
+        s_status[w] = st;
+    }
 }
 
 enum ChunkMode : uint32_t { MODE_NONE = 0, MODE_COPY = 1, MODE_WALK = 2 };
@@ -619,6 +749,14 @@ uint32_t chains_per_wave() { // A/B: ZDBCRC_CHAINS_PER_WAVE (1..64)
     return v;
 }
 
+int chain_mode() { // A/B: ZDBCRC_CHAIN_MODE (0: one lane per chunk, 1: one wave per chunk, 1 KiB windows)
+    static const int v = [] {
+        const char *e = std::getenv("ZDBCRC_CHAIN_MODE");
+        return e ? std::atoi(e) : -1;
+    }();
+    return v;
+}
+
 int search_variant() {
     static const int v = [] {
         const char *e = std::getenv("ZDBCRC_SEARCH_VARIANT");
@@ -711,9 +849,14 @@ int zdb_datafile_walk_device(const uint8_t *d_image, const uint64_t *d_file_off,
     case 6: hipLaunchKernelGGL((walk_search_kernel<256, 8, true>), dim3((uint32_t)nchunks), dim3(256), 0, st, t, s_start, s_status); break;
     case 7: hipLaunchKernelGGL((walk_search_kernel<256, 16, true>), dim3((uint32_t)nchunks), dim3(256), 0, st, t, s_start, s_status); break;
     case 8: hipLaunchKernelGGL((walk_search_kernel<128, 16, true>), dim3((uint32_t)nchunks), dim3(128), 0, st, t, s_start, s_status); break;
+    // occupancy: at most 64 / 80 VGPRs (8 / 6 waves per SIMD; the default shape takes 82 -> 5)
+    case 10: hipLaunchKernelGGL((walk_search_kernel<256, 8, true, 8>), dim3((uint32_t)nchunks), dim3(256), 0, st, t, s_start, s_status); break;
+    case 11: hipLaunchKernelGGL((walk_search_kernel<256, 4, true, 8>), dim3((uint32_t)nchunks), dim3(256), 0, st, t, s_start, s_status); break;
+    case 12: hipLaunchKernelGGL((walk_search_kernel<256, 8, true, 6>), dim3((uint32_t)nchunks), dim3(256), 0, st, t, s_start, s_status); break;
+    case 13: hipLaunchKernelGGL((walk_search_kernel<128, 8, true, 8>), dim3((uint32_t)nchunks), dim3(128), 0, st, t, s_start, s_status); break;
     default:
 #endif
-    hipLaunchKernelGGL((walk_search_kernel<SEARCH_T, SEARCH_SU, true>), dim3((uint32_t)nchunks), dim3(SEARCH_T), 0,
+    hipLaunchKernelGGL((walk_search_kernel<SEARCH_T, SEARCH_SU, true, SEARCH_MW>), dim3((uint32_t)nchunks), dim3(SEARCH_T), 0,
                        st, t, s_start, s_status);
 #ifdef ZDBCRC_DIAG
     }
@@ -724,8 +867,17 @@ int zdb_datafile_walk_device(const uint8_t *d_image, const uint64_t *d_file_off,
     const uint32_t cpw = CHAINS_PER_WAVE;
 #endif
     const dim3 gchain((uint32_t)((nchunks + cpw - 1) / cpw));
-    hipLaunchKernelGGL(walk_spec_kernel, gchain, dim3(64), 0, st, t, s_start, s_exit, s_count, s_status, slots,
-                       kcap, cpw);
+#ifdef ZDBCRC_DIAG
+    const bool win_chain = chain_mode() >= 0 ? chain_mode() == 1 : WINDOW_CHAIN;
+#else
+    const bool win_chain = WINDOW_CHAIN;
+#endif
+    if (win_chain)
+        hipLaunchKernelGGL(walk_spec_win_kernel, dim3((uint32_t)nchunks), dim3(64), 0, st, t, s_start, s_exit,
+                           s_count, s_status, slots, kcap);
+    else
+        hipLaunchKernelGGL(walk_spec_kernel, gchain, dim3(64), 0, st, t, s_start, s_exit, s_count, s_status, slots,
+                           kcap, cpw);
     hipLaunchKernelGGL(walk_stitch_kernel, dim3((nfiles + WALK_T - 1) / WALK_T), dim3(WALK_T), 0, st, t, s_start,
                        s_exit, s_count, s_status, true_start, chunk_base, chunk_mode, kcap, d_file_records,
                        d_file_status, d_rewalks);

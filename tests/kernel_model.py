@@ -18,8 +18,10 @@ LDS_DW = OFF_L + SCH * 32 * WAVE
 OFF_Z = LDS_DW
 OFF_R = OFF_Z + 16 * SCH * 32
 RDIG = 4
-TABLE_DW = OFF_R + RDIG * 256 * SCH * 32
+OFF_F = OFF_R + RDIG * 256 * SCH * 32
+TABLE_DW = OFF_F + 4 * SCH * 32
 UNIT_OVH = 384
+DWG_MIN_BYTES = 64 * 1024  # record-relative grids this long load from the dword below the record
 MIN_UNITS_PER_WAVE = 256
 
 LANES = np.arange(WAVE, dtype=np.int64)
@@ -188,11 +190,17 @@ def batch(arena: np.ndarray, offsets, lengths, tab: np.ndarray, max_waves: int =
                 aend = a + int(lengths[r])
                 np_ = ur - us
                 rel = np_ != pieces_aligned(a, aend - a)
-                P0 = a if rel else a & ~15
-                z = P0 + 16 * np_ - aend
+                h = a & 3 if rel and aend - a >= DWG_MIN_BYTES else 0  # loads from the dword below
+                P0 = a - h if rel else a & ~15
+                z = 0 if rel else P0 + 16 * np_ - aend
                 pa, pb = s_lo - us, s_hi - us
-                x = segment_crc(mem, mem_base, P0, pa, pb, np_, 0 if rel else a & 15, 16 - z, tab)
-                if z:
+                x = segment_crc(mem, mem_base, P0, pa, pb, np_, h if rel else a & 15, 16 - z, tab)
+                if h:  # the record's last h bytes: crc(X || y) = shift(crc(X) ^ y, h)
+                    y = 0
+                    if pb == np_:
+                        y = int.from_bytes(mem[aend - h - mem_base:aend - mem_base].tobytes(), "little")
+                    x = _uniform_shift(x ^ y, tab, OFF_F + h * SCH * 32)
+                elif z:
                     x = _uniform_shift(x, tab, OFF_Z + z * SCH * 32)
                 x = shift_pieces(x, np_ - pb, tab)
                 out[r] ^= np.uint32(x)  # store for whole records == xor into 0

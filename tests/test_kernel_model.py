@@ -96,9 +96,20 @@ def test_record_relative_grid(oracle_c, tab):
     for r, (o, L) in enumerate(zip(offs, lens)):
         if L % 1024 == 0 and o % 16:
             assert km.record_pieces(o, L) == L // 16 < km.pieces_aligned(o, L)
-    for mw, mu in ((4096, 256), (7, 1)):
-        got = km.batch(arena, offs, lens, tab, max_waves=mw, min_units=mu)
-        np.testing.assert_array_equal(got, oracle_c.batch(arena, offs, lens))
+    # records of 64 KiB and more: loads start at the dword below the record
+    # (h = A mod 4 bytes masked, the last h bytes folded in at the end)
+    big = oracle.splitmix_bytes(300_000, 34)
+    blens = [65536, 1024, 131072, 65536 + 16]
+    boffs = [13, 65600, 66627, 197710]
+    assert all(km.record_pieces(o, L) == L // 16 for o, L in zip(boffs, blens) if L % 1024 == 0)
+    for base in (0, 1, 2, 3):
+        for mw, mu in ((4096, 256), (9, 1)):
+            got = km.batch(big, boffs, blens, tab, max_waves=mw, min_units=mu, base_addr=base)
+            np.testing.assert_array_equal(got, oracle_c.batch(big, boffs, blens))
+    for base in (0, 1, 2, 3):
+        for mw, mu in ((4096, 256), (7, 1)):
+            got = km.batch(arena, offs, lens, tab, max_waves=mw, min_units=mu, base_addr=base)
+            np.testing.assert_array_equal(got, oracle_c.batch(arena, offs, lens))
 
 
 @pytest.mark.parametrize("dyn,cpw,pools", [(6, 4, 4), (8, 3, 2), (16, 1, 1), (2, 5, 4)])
