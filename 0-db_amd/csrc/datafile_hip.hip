@@ -80,6 +80,10 @@ constexpr uint32_t CHAINS_PER_WAVE = 16;
 // instead of one lane per chunk reading each header (C4: walk -1.5 to -3 %
 // in two A/B rounds, the same records and exits: GPU walk tests)
 constexpr bool WINDOW_CHAIN = true;
+// A1 + A2 fused (walk_search_chain_kernel): a chunk's chain starts as soon as
+// its own search is done, overlapping the other chunks' searches (C4 walk
+// 0.482 -> 0.421 ms in two A/B rounds, profiles/r2/walk_fused_ab.jsonl)
+constexpr bool FUSED_WALK = true;
 
 // little-endian u32 at any byte address: two aligned dword loads + one
 // v_alignbyte (reads up to 7 bytes past p; images are readable 16 bytes past
@@ -362,37 +366,32 @@ __device__ __forceinline__ uint64_t scan_block(const uint8_t *f, uint64_t len, u
 // not (most bytes are in the large values), uniformly within it, so the
 // nearer of the two ends is found in half the scanning on average and in
 // the worst case.
-template <int NT, int SU, bool NOA1 = false, int MW = 1>
-__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MW))) void walk_search_kernel(FileTab t, uint64_t *__restrict__ s_start,
-                                                         int32_t *__restrict__ s_status) {
+// the search of chunk w (one workgroup of NT threads); every thread returns
+// the chunk's speculative start and status
+template <int NT, int SU, bool NOA1>
+__device__ __forceinline__ void search_chunk(const FileTab &t, uint64_t w, uint64_t &start, int32_t &status) {
     constexpr uint32_t NWS = NT / 64, NF = NWS / 2, NB = NWS - NF;
     constexpr uint64_t SB = 1024u * SU; // bytes per wave block
     __shared__ unsigned long long bestf;
     __shared__ unsigned int bestb;
     const uint32_t lane = threadIdx.x & 63u, wid = threadIdx.x >> 6;
-    const uint64_t w = blockIdx.x;
     const uint32_t fi = (uint32_t)(w / t.cpf), c = (uint32_t)(w % t.cpf);
     const uint64_t len = t.file_len[fi];
     const uint8_t *f = t.image + t.file_off[fi];
     const uint64_t C = 1ull << t.lg, c0 = (uint64_t)c * C;
+    status = ST_CONTINUE;
     if (c == 0) {
-        if (threadIdx.x == 0) {
-            // data_descriptor_load / _validate (data.c:177-209): 28-byte
-            // header, magic "DAT0", version 3
-            const bool bad = len < ZDB_DATA_HEADER_SIZE || f[0] != 'D' || f[1] != 'A' || f[2] != 'T' ||
-                             f[3] != '0' || ld_le32(f + 4) != ZDB_DATAFILE_VERSION;
-            s_start[w] = bad ? NONE : (uint64_t)ZDB_DATA_HEADER_SIZE;
-            s_status[w] = bad ? ZDB_WALK_BAD_DESCRIPTOR : ST_CONTINUE;
-        }
+        // data_descriptor_load / _validate (data.c:177-209): 28-byte
+        // header, magic "DAT0", version 3
+        const bool bad = len < ZDB_DATA_HEADER_SIZE || f[0] != 'D' || f[1] != 'A' || f[2] != 'T' ||
+                         f[3] != '0' || ld_le32(f + 4) != ZDB_DATAFILE_VERSION;
+        start = bad ? NONE : (uint64_t)ZDB_DATA_HEADER_SIZE;
+        status = bad ? ZDB_WALK_BAD_DESCRIPTOR : ST_CONTINUE;
         return;
     }
-    if (c0 >= len || len < ZDB_ENTRY_HEADER_SIZE) {
-        if (threadIdx.x == 0) {
-            s_start[w] = NONE;
-            s_status[w] = ST_CONTINUE;
-        }
+    start = NONE;
+    if (c0 >= len || len < ZDB_ENTRY_HEADER_SIZE)
         return;
-    }
     // positions p in [c0, c0 + C) with a whole 18-byte header in the file
     const uint64_t lim = (c0 + C < len - (ZDB_ENTRY_HEADER_SIZE - 1)) ? c0 + C : len - (ZDB_ENTRY_HEADER_SIZE - 1);
     constexpr uint64_t LO = ZDB_DATA_HEADER_SIZE; // entries start at or after the datafile header
@@ -443,12 +442,21 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MW))) void w
         if (back && (k + 1) * NB * SB >= c0 + SB - LO)
             back = false; // reached the datafile header
         if (done) {
-            if (threadIdx.x == 0) {
-                s_start[w] = ans;
-                s_status[w] = ST_CONTINUE;
-            }
+            start = ans;
             return;
         }
+    }
+}
+
+template <int NT, int SU, bool NOA1 = false, int MW = 1>
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MW))) void walk_search_kernel(
+    FileTab t, uint64_t *__restrict__ s_start, int32_t *__restrict__ s_status) {
+    uint64_t start;
+    int32_t status;
+    search_chunk<NT, SU, NOA1>(t, blockIdx.x, start, status);
+    if (threadIdx.x == 0) {
+        s_start[blockIdx.x] = start;
+        s_status[blockIdx.x] = status;
     }
 }
 
@@ -536,16 +544,11 @@ __device__ __forceinline__ bool in_window(const Window &w, const uint8_t *f, uin
     return reinterpret_cast<uintptr_t>(f + pos) - w.base + 13u <= 1024u;
 }
 
-__global__ __launch_bounds__(64) void walk_spec_win_kernel(FileTab t, const uint64_t *__restrict__ s_start,
-                                                           uint64_t *__restrict__ s_exit,
-                                                           uint32_t *__restrict__ s_count,
-                                                           int32_t *__restrict__ s_status, RecSlot *__restrict__ slots,
-                                                           uint32_t kcap) {
-    const uint64_t w = blockIdx.x;
-    const uint32_t lane = threadIdx.x;
-    const uint64_t start = s_start[w];
-    if (start == NONE)
-        return;
+// the windowed chain of chunk w from its speculative start (one wave)
+__device__ __forceinline__ void chain_window(const FileTab &t, uint64_t w, uint64_t start, uint32_t lane,
+                                             uint64_t *__restrict__ s_exit, uint32_t *__restrict__ s_count,
+                                             int32_t *__restrict__ s_status, RecSlot *__restrict__ slots,
+                                             uint32_t kcap) {
     const uint32_t fi = (uint32_t)(w / t.cpf), c = (uint32_t)(w % t.cpf);
     const uint64_t len = t.file_len[fi];
     const uint8_t *f = t.image + t.file_off[fi];
@@ -600,6 +603,35 @@ __global__ __launch_bounds__(64) void walk_spec_win_kernel(FileTab t, const uint
         s_count[w] = count;
         s_status[w] = st;
     }
+}
+
+__global__ __launch_bounds__(64) void walk_spec_win_kernel(FileTab t, const uint64_t *__restrict__ s_start,
+                                                           uint64_t *__restrict__ s_exit,
+                                                           uint32_t *__restrict__ s_count,
+                                                           int32_t *__restrict__ s_status, RecSlot *__restrict__ slots,
+                                                           uint32_t kcap) {
+    const uint64_t start = s_start[blockIdx.x];
+    if (start != NONE)
+        chain_window(t, blockIdx.x, start, threadIdx.x, s_exit, s_count, s_status, slots, kcap);
+}
+
+// A1 + A2 in one kernel: the first wave of a chunk's search workgroup follows
+// the chunk's chain as soon as its start is known, so the chains' round trips
+// overlap the searches of the other chunks (and the next workgroups' start)
+// instead of following all of them
+template <int NT, int SU, int MW>
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MW))) void walk_search_chain_kernel(
+    FileTab t, uint64_t *__restrict__ s_start, int32_t *__restrict__ s_status, uint64_t *__restrict__ s_exit,
+    uint32_t *__restrict__ s_count, RecSlot *__restrict__ slots, uint32_t kcap) {
+    uint64_t start;
+    int32_t status;
+    search_chunk<NT, SU, true>(t, blockIdx.x, start, status);
+    if (threadIdx.x == 0) {
+        s_start[blockIdx.x] = start;
+        s_status[blockIdx.x] = status;
+    }
+    if (threadIdx.x < 64 && start != NONE)
+        chain_window(t, blockIdx.x, start, threadIdx.x, s_exit, s_count, s_status, slots, kcap);
 }
 
 enum ChunkMode : uint32_t { MODE_NONE = 0, MODE_COPY = 1, MODE_WALK = 2 };
@@ -749,7 +781,8 @@ uint32_t chains_per_wave() { // A/B: ZDBCRC_CHAINS_PER_WAVE (1..64)
     return v;
 }
 
-int chain_mode() { // A/B: ZDBCRC_CHAIN_MODE (0: one lane per chunk, 1: one wave per chunk, 1 KiB windows)
+int chain_mode() { // A/B: ZDBCRC_CHAIN_MODE (0: one lane per chunk, 1: one wave per chunk, 1 KiB windows,
+                   // 2: the windowed chain fused into the search kernel)
     static const int v = [] {
         const char *e = std::getenv("ZDBCRC_CHAIN_MODE");
         return e ? std::atoi(e) : -1;
@@ -839,6 +872,21 @@ int zdb_datafile_walk_device(const uint8_t *d_image, const uint64_t *d_file_off,
 
     const FileTab t{d_image, d_file_off, d_file_len, nfiles, (uint32_t)cpf64, lg};
 #ifdef ZDBCRC_DIAG
+    const uint32_t cpw = chains_per_wave();
+#else
+    const uint32_t cpw = CHAINS_PER_WAVE;
+#endif
+    const dim3 gchain((uint32_t)((nchunks + cpw - 1) / cpw));
+#ifdef ZDBCRC_DIAG
+    const bool fused = chain_mode() >= 0 ? chain_mode() == 2 : FUSED_WALK;
+#else
+    const bool fused = FUSED_WALK;
+#endif
+    if (fused)
+        hipLaunchKernelGGL((walk_search_chain_kernel<SEARCH_T, SEARCH_SU, SEARCH_MW>), dim3((uint32_t)nchunks),
+                           dim3(SEARCH_T), 0, st, t, s_start, s_status, s_exit, s_count, slots, kcap);
+    else {
+#ifdef ZDBCRC_DIAG
     switch (search_variant()) { // A/B (scripts/walk_probe.py with the diagnostic library)
     case 9: hipLaunchKernelGGL((walk_search_kernel<256, 8, false>), dim3((uint32_t)nchunks), dim3(256), 0, st, t, s_start, s_status); break;
     case 1: hipLaunchKernelGGL((walk_search_kernel<128, 8>), dim3((uint32_t)nchunks), dim3(128), 0, st, t, s_start, s_status); break;
@@ -862,12 +910,6 @@ int zdb_datafile_walk_device(const uint8_t *d_image, const uint64_t *d_file_off,
     }
 #endif
 #ifdef ZDBCRC_DIAG
-    const uint32_t cpw = chains_per_wave();
-#else
-    const uint32_t cpw = CHAINS_PER_WAVE;
-#endif
-    const dim3 gchain((uint32_t)((nchunks + cpw - 1) / cpw));
-#ifdef ZDBCRC_DIAG
     const bool win_chain = chain_mode() >= 0 ? chain_mode() == 1 : WINDOW_CHAIN;
 #else
     const bool win_chain = WINDOW_CHAIN;
@@ -878,6 +920,7 @@ int zdb_datafile_walk_device(const uint8_t *d_image, const uint64_t *d_file_off,
     else
         hipLaunchKernelGGL(walk_spec_kernel, gchain, dim3(64), 0, st, t, s_start, s_exit, s_count, s_status, slots,
                            kcap, cpw);
+    } // not fused
     hipLaunchKernelGGL(walk_stitch_kernel, dim3((nfiles + WALK_T - 1) / WALK_T), dim3(WALK_T), 0, st, t, s_start,
                        s_exit, s_count, s_status, true_start, chunk_base, chunk_mode, kcap, d_file_records,
                        d_file_status, d_rewalks);
