@@ -658,7 +658,11 @@ def cpu_rank(args, rank: int, world: int) -> None:
     the timing and aggregation are the GPU path's (combine_ranks)."""
     import torch.distributed as dist
     import zdbcrc
+    result_out = sys.stdout  # one JSON line on stdout (see main)
     if world > 1:
+        sys.stdout.flush()
+        result_out = os.fdopen(os.dup(1), "w")
+        os.dup2(2, 1)
         dist.init_process_group("gloo")
     target = int(args.gib * (1 << 30))
     offs, lens, seed, desc = make_dataset(args.workload, target, rank)
@@ -685,7 +689,7 @@ def cpu_rank(args, rank: int, world: int) -> None:
             "vs_baseline": None, "dtype": "u8", "data": "synthetic", "device": "cpu (plumbing test: scalar engine)",
             "config": {"workload": desc, "records_per_gpu": len(lens), "payload_bytes_per_gpu": payload,
                        "parallelism": f"{world} independent shards, no data-path collective"},
-            "parity": summarize_parity(parities), "parity_by_rank": parities}), flush=True)
+            "parity": summarize_parity(parities), "parity_by_rank": parities}), file=result_out, flush=True)
     if world > 1:
         dist.destroy_process_group()
 
@@ -731,7 +735,14 @@ def main():
     ndev = torch.cuda.device_count()
     local = local % max(ndev, 1)
     torch.cuda.set_device(local)
+    # stdout carries exactly one JSON line: the communication libraries print
+    # their connection chatter on fd 1 (gloo: "Rank 0 is connected to 1 peer
+    # ranks"), so fd 1 goes to stderr and the result line to the original stdout
+    result_out = sys.stdout
     if world > 1:
+        sys.stdout.flush()
+        result_out = os.fdopen(os.dup(1), "w")
+        os.dup2(2, 1)
         if world <= ndev:
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:
@@ -872,7 +883,7 @@ def main():
                        "parallelism": f"{world} independent shards, no data-path collective"},
             "parity": summarize_parity(parities), "parity_by_rank": parities, "roofline": roofline, "cpu_baseline": cpu, "extra": extra,
         }
-        print(json.dumps(line), flush=True)
+        print(json.dumps(line), file=result_out, flush=True)
     if world > 1:
         dist.destroy_process_group()
 
