@@ -638,19 +638,13 @@ enum ChunkMode : uint32_t { MODE_NONE = 0, MODE_COPY = 1, MODE_WALK = 2 };
 
 // B: exact stitch (one thread per file); re-walks a chunk serially when its
 // speculative start is not the true exit of the chunk before it
-__global__ __launch_bounds__(WALK_T) void walk_stitch_kernel(FileTab t, const uint64_t *__restrict__ s_start,
-                                                             const uint64_t *__restrict__ s_exit,
-                                                             const uint32_t *__restrict__ s_count,
-                                                             const int32_t *__restrict__ s_status,
-                                                             uint64_t *__restrict__ true_start,
-                                                             uint64_t *__restrict__ chunk_base,
-                                                             uint32_t *__restrict__ chunk_mode, uint32_t kcap,
-                                                             uint64_t *__restrict__ file_records,
-                                                             int32_t *__restrict__ file_status,
-                                                             uint32_t *__restrict__ rewalks) {
-    const uint32_t fi = blockIdx.x * WALK_T + threadIdx.x;
-    if (fi >= t.nfiles)
-        return;
+// the exact stitch of one file (see walk_stitch_kernel)
+__device__ __forceinline__ void stitch_file(const FileTab &t, uint32_t fi, const uint64_t *__restrict__ s_start,
+                                            const uint64_t *__restrict__ s_exit, const uint32_t *__restrict__ s_count,
+                                            const int32_t *__restrict__ s_status, uint64_t *__restrict__ true_start,
+                                            uint64_t *__restrict__ chunk_base, uint32_t *__restrict__ chunk_mode,
+                                            uint32_t kcap, uint64_t *__restrict__ file_records,
+                                            int32_t *__restrict__ file_status, uint32_t *__restrict__ rewalks) {
     const uint64_t len = t.file_len[fi];
     const uint8_t *f = t.image + t.file_off[fi];
     const uint64_t w0 = (uint64_t)fi * t.cpf;
@@ -698,6 +692,37 @@ __global__ __launch_bounds__(WALK_T) void walk_stitch_kernel(FileTab t, const ui
     rewalks[fi] = redo;
 }
 
+__global__ __launch_bounds__(WALK_T) void walk_stitch_kernel(FileTab t, const uint64_t *__restrict__ s_start,
+                                                             const uint64_t *__restrict__ s_exit,
+                                                             const uint32_t *__restrict__ s_count,
+                                                             const int32_t *__restrict__ s_status,
+                                                             uint64_t *__restrict__ true_start,
+                                                             uint64_t *__restrict__ chunk_base,
+                                                             uint32_t *__restrict__ chunk_mode, uint32_t kcap,
+                                                             uint64_t *__restrict__ file_records,
+                                                             int32_t *__restrict__ file_status,
+                                                             uint32_t *__restrict__ rewalks, bool prefix) {
+    const uint32_t fi = blockIdx.x * WALK_T + threadIdx.x;
+    if (fi < t.nfiles)
+        stitch_file(t, fi, s_start, s_exit, s_count, s_status, true_start, chunk_base, chunk_mode, kcap, file_records,
+                    file_status, rewalks);
+    if (prefix) { // one block holds every file: the file prefix here instead of walk_prefix_kernel
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            uint64_t acc = 0;
+            uint32_t redo = 0;
+            for (uint32_t i = 0; i < t.nfiles; i++) {
+                const uint64_t n = file_records[i];
+                file_records[i] = acc;
+                acc += n;
+                redo += rewalks[i];
+            }
+            file_records[t.nfiles] = acc;
+            rewalks[t.nfiles] = redo;
+        }
+    }
+}
+
 // B2: record counts -> global record base of every file, in place
 // (exclusive prefix; entry nfiles = total)
 __global__ void walk_prefix_kernel(uint32_t nfiles, uint64_t *__restrict__ file_records,
@@ -718,15 +743,13 @@ __global__ void walk_prefix_kernel(uint32_t nfiles, uint64_t *__restrict__ file_
 
 // C1: descriptors of the accepted chunks, copied from their slots (one
 // thread per slot)
-__global__ __launch_bounds__(WALK_T) void walk_copy_kernel(FileTab t, const uint32_t *__restrict__ chunk_mode,
-                                                           const uint32_t *__restrict__ s_count,
-                                                           const RecSlot *__restrict__ slots, uint32_t kcap,
-                                                           const uint64_t *__restrict__ chunk_base,
-                                                           const uint64_t *__restrict__ file_base, uint64_t capacity,
-                                                           uint64_t *__restrict__ entry_off, uint64_t *__restrict__ poff,
-                                                           uint32_t *__restrict__ plen,
-                                                           uint32_t *__restrict__ expect) {
-    const uint64_t g = (uint64_t)blockIdx.x * WALK_T + threadIdx.x;
+// slot g of the accepted chunks -> its final descriptor (C1)
+__device__ __forceinline__ void copy_slot(const FileTab &t, uint64_t g, const uint32_t *__restrict__ chunk_mode,
+                                          const uint32_t *__restrict__ s_count, const RecSlot *__restrict__ slots,
+                                          uint32_t kcap, const uint64_t *__restrict__ chunk_base,
+                                          const uint64_t *__restrict__ file_base, uint64_t capacity,
+                                          uint64_t *__restrict__ entry_off, uint64_t *__restrict__ poff,
+                                          uint32_t *__restrict__ plen, uint32_t *__restrict__ expect) {
     const uint64_t w = g / kcap;
     const uint32_t i = (uint32_t)(g % kcap);
     if (w >= (uint64_t)t.nfiles * t.cpf || chunk_mode[w] != MODE_COPY || i >= s_count[w])
@@ -746,15 +769,15 @@ __global__ __launch_bounds__(WALK_T) void walk_copy_kernel(FileTab t, const uint
 // C2: descriptors of the chunks that had to be re-walked, or had more
 // records than slots (one lane per chunk, CHAINS_PER_WAVE per one-wave
 // workgroup, as A2)
-__global__ __launch_bounds__(64) void walk_emit_kernel(FileTab t, const uint64_t *__restrict__ true_start,
-                                                       const uint32_t *__restrict__ chunk_mode,
-                                                       const uint64_t *__restrict__ chunk_base,
-                                                       const uint64_t *__restrict__ file_base, uint64_t capacity,
-                                                       uint64_t *__restrict__ entry_off, uint64_t *__restrict__ poff,
-                                                       uint32_t *__restrict__ plen, uint32_t *__restrict__ expect,
-                                                       uint32_t cpw) {
-    const uint64_t w = (uint64_t)blockIdx.x * cpw + threadIdx.x;
-    if (threadIdx.x >= cpw || w >= (uint64_t)t.nfiles * t.cpf || chunk_mode[w] != MODE_WALK)
+// chunk w, when it was re-walked or overflowed its slots: a serial walk
+// writes its descriptors (C2)
+__device__ __forceinline__ void emit_chunk(const FileTab &t, uint64_t w, const uint64_t *__restrict__ true_start,
+                                           const uint32_t *__restrict__ chunk_mode,
+                                           const uint64_t *__restrict__ chunk_base,
+                                           const uint64_t *__restrict__ file_base, uint64_t capacity,
+                                           uint64_t *__restrict__ entry_off, uint64_t *__restrict__ poff,
+                                           uint32_t *__restrict__ plen, uint32_t *__restrict__ expect) {
+    if (w >= (uint64_t)t.nfiles * t.cpf || chunk_mode[w] != MODE_WALK)
         return;
     const uint32_t fi = (uint32_t)(w / t.cpf), c = (uint32_t)(w % t.cpf);
     const uint64_t cend = ((uint64_t)c + 1) << t.lg;
@@ -764,6 +787,25 @@ __global__ __launch_bounds__(64) void walk_emit_kernel(FileTab t, const uint64_t
     int32_t st;
     walk_chain<EMIT>(t.image + foff, t.file_len[fi], true_start[w], cend, count, exit, st, nullptr, 0, foff,
                      file_base[fi] + chunk_base[w], capacity, entry_off, poff, plen, expect);
+}
+
+// C1 + C2 in one launch: blocks [0, ncopy) copy the slots of accepted chunks,
+// the blocks after them emit the re-walked ones (one chunk per thread; rare)
+__global__ __launch_bounds__(WALK_T) void walk_out_kernel(FileTab t, const uint64_t *__restrict__ true_start,
+                                                          const uint32_t *__restrict__ chunk_mode,
+                                                          const uint32_t *__restrict__ s_count,
+                                                          const RecSlot *__restrict__ slots, uint32_t kcap,
+                                                          const uint64_t *__restrict__ chunk_base,
+                                                          const uint64_t *__restrict__ file_base, uint64_t capacity,
+                                                          uint64_t *__restrict__ entry_off, uint64_t *__restrict__ poff,
+                                                          uint32_t *__restrict__ plen, uint32_t *__restrict__ expect,
+                                                          uint32_t ncopy) {
+    if (blockIdx.x < ncopy)
+        copy_slot(t, (uint64_t)blockIdx.x * WALK_T + threadIdx.x, chunk_mode, s_count, slots, kcap, chunk_base,
+                  file_base, capacity, entry_off, poff, plen, expect);
+    else
+        emit_chunk(t, (uint64_t)(blockIdx.x - ncopy) * WALK_T + threadIdx.x, true_start, chunk_mode, chunk_base,
+                   file_base, capacity, entry_off, poff, plen, expect);
 }
 
 #ifdef ZDBCRC_DIAG
@@ -921,17 +963,17 @@ int zdb_datafile_walk_device(const uint8_t *d_image, const uint64_t *d_file_off,
         hipLaunchKernelGGL(walk_spec_kernel, gchain, dim3(64), 0, st, t, s_start, s_exit, s_count, s_status, slots,
                            kcap, cpw);
     } // not fused
+    const bool one_block = nfiles <= WALK_T; // stitch and file prefix in one launch
     hipLaunchKernelGGL(walk_stitch_kernel, dim3((nfiles + WALK_T - 1) / WALK_T), dim3(WALK_T), 0, st, t, s_start,
                        s_exit, s_count, s_status, true_start, chunk_base, chunk_mode, kcap, d_file_records,
-                       d_file_status, d_rewalks);
-    hipLaunchKernelGGL(walk_prefix_kernel, dim3(1), dim3(64), 0, st, nfiles, d_file_records, d_rewalks);
+                       d_file_status, d_rewalks, one_block);
+    if (!one_block)
+        hipLaunchKernelGGL(walk_prefix_kernel, dim3(1), dim3(64), 0, st, nfiles, d_file_records, d_rewalks);
     if (capacity) {
-        const uint64_t nslots = nchunks * kcap;
-        hipLaunchKernelGGL(walk_copy_kernel, dim3((uint32_t)((nslots + WALK_T - 1) / WALK_T)), dim3(WALK_T), 0, st,
-                           t, chunk_mode, s_count, slots, kcap, chunk_base, d_file_records, capacity, d_entry_off,
-                           d_payload_off, d_payload_len, d_expected);
-        hipLaunchKernelGGL(walk_emit_kernel, gchain, dim3(64), 0, st, t, true_start, chunk_mode, chunk_base,
-                           d_file_records, capacity, d_entry_off, d_payload_off, d_payload_len, d_expected, cpw);
+        const uint64_t ncopy = (nchunks * kcap + WALK_T - 1) / WALK_T, nemit = (nchunks + WALK_T - 1) / WALK_T;
+        hipLaunchKernelGGL(walk_out_kernel, dim3((uint32_t)(ncopy + nemit)), dim3(WALK_T), 0, st, t, true_start,
+                           chunk_mode, s_count, slots, kcap, chunk_base, d_file_records, capacity, d_entry_off,
+                           d_payload_off, d_payload_len, d_expected, (uint32_t)ncopy);
     }
     return hipGetLastError() == hipSuccess ? ZDB_CRC32_OK : ZDB_CRC32_ELAUNCH;
 }
