@@ -590,7 +590,7 @@ __device__ __forceinline__ uint64_t block_excl_scan64(uint64_t v, uint64_t *wsum
 // are flushed with atomic XOR at each claim (at most 2 are pending then).
 template <int WGT, int WPE, bool STAMP = false, int PRIO = 0, uint32_t UO = UNIT_OVH, int NOZ = 0,
           bool NTL = false, bool NOLOAD = false, int XM = 0, int DYN = 0, int CPW = 4, uint32_t DYN_POOLS = 8,
-          bool SP = false, int PP = 0, bool SEGDUMP = false, bool BMG = false>
+          bool SP = false, int PP = 0, bool SEGDUMP = false, bool BMG = false, bool XP = false>
 __global__ __launch_bounds__(WGT, WPE) void crc_batch_kernel_v3(
     const uint8_t *__restrict__ arena, const uint64_t *__restrict__ offsets,
     const uint32_t *__restrict__ lengths, const PlanArgs plan, uint64_t n,
@@ -707,7 +707,9 @@ __global__ __launch_bounds__(WGT, WPE) void crc_batch_kernel_v3(
     uint32_t cut_x[2] = {0, 0}, ncut = 0;
     uint64_t pbase = 0; // units of earlier ranges (PRIO progress)
     // tail pool of this workgroup: chunk c covers [P0 + PL c / nch, P0 + PL (c+1) / nch)
-    const uint32_t pool = blockIdx.x % DYN_POOLS;
+    // XP: the workgroups of a pool come from every XCD (workgroup b runs on XCD
+    // b mod 8), so that a slower XCD's share of the pool is taken by the others
+    const uint32_t pool = (XP ? blockIdx.x >> 3 : blockIdx.x) % DYN_POOLS;
     const uint64_t Td = total - Ts;
     const uint64_t P0 = Ts + Td * pool / DYN_POOLS;
     const uint64_t PL = Ts + Td * (pool + 1) / DYN_POOLS - P0;
@@ -919,7 +921,7 @@ struct KernelVariant {
 // several of which compute wrong checksums by design (NOZ, NOLOAD, XM);
 // selectable with ZDBCRC_VARIANT=<index> or zdbcrc_debug_set_variant
 const KernelVariant kVariants[] = {
-    {"v3_wg768_nt_dyn4c4p32_sp", crc_batch_kernel_v3<768, 6, false, 0, UNIT_OVH, false, true, false, 0, 4, 4, 32, true>, 768},
+    {"v3_wg768_nt_dyn4c4p32_sp_xp", crc_batch_kernel_v3<768, 6, false, 0, UNIT_OVH, false, true, false, 0, 4, 4, 32, true, 0, false, false, true>, 768},
     {"v3_wg768_nt_dyn6c4p32", crc_batch_kernel_v3<768, 6, false, 0, UNIT_OVH, false, true, false, 0, 6, 4, 32>, 768},
     {"v3_wg768_prio_nt", crc_batch_kernel_v3<768, 6, false, 1, UNIT_OVH, false, true>, 768},
     {"v3_wg768_prio", crc_batch_kernel_v3<768, 6, false, 1>, 768},
@@ -954,6 +956,11 @@ const KernelVariant kVariants[] = {
     // default's loads from the dword below the record
     {"v3_wg768_nt_dyn4c4p32_sp_bmg", crc_batch_kernel_v3<768, 6, false, 0, UNIT_OVH, false, true, false, 0, 4, 4, 32, true, 0, false, true>, 768},
     {"v3_wg768_nt_dyn4c4p32_sp_pp_wait_bmg", crc_batch_kernel_v3<768, 6, false, 0, UNIT_OVH, false, true, false, 0, 4, 4, 32, true, 3, false, true>, 768},
+    // round 2: tail pools drawn from every XCD (XP; index 0 is the product default with XP, this
+    // the default before it)
+    {"v3_wg768_nt_dyn4c4p32_sp", crc_batch_kernel_v3<768, 6, false, 0, UNIT_OVH, false, true, false, 0, 4, 4, 32, true>, 768},
+    {"v3_wg768_nt_dyn4c4p32_sp_pp_wait_bmg_xp", crc_batch_kernel_v3<768, 6, false, 0, UNIT_OVH, false, true, false, 0, 4, 4, 32, true, 3, false, true, true>, 768},
+    {"v3_wg768_nt_dyn4c4p32_sp_stamp_xp", crc_batch_kernel_v3<768, 6, true, 0, UNIT_OVH, false, true, false, 0, 4, 4, 32, true, 0, false, false, true>, 768},
     // round 2, after the dword grid: planning charge and pool share re-checked
     {"v3_wg768_nt_dyn4c4p32_sp_uo256", crc_batch_kernel_v3<768, 6, false, 0, 256, false, true, false, 0, 4, 4, 32, true>, 768, WG_PER_CU, 256},
     {"v3_wg768_nt_dyn4c4p32_sp_uo512", crc_batch_kernel_v3<768, 6, false, 0, 512, false, true, false, 0, 4, 4, 32, true>, 768, WG_PER_CU, 512},
@@ -977,8 +984,9 @@ const KernelVariant &variant(bool /*small: the A/B harness picks by index*/ = fa
 }
 #else
 // the product library ships the checksum kernel in two loop shapes, no
-// environment knob: tail pool (4/16 of the units, 32 pools, 4 chunks per
-// wave) with static-phase priority, 768 threads, nontemporal payload loads
+// environment knob: tail pool (4/16 of the units, 32 pools drawn from every
+// XCD, 4 chunks per wave) with static-phase priority, 768 threads,
+// nontemporal payload loads
 // (DESIGN.md §4.1); the small-record shape (PP 3: the loop unrolled twice,
 // load buffers swapping roles instead of 16 register copies per superstep,
 // the next loads issued once the previous ones have landed) for batches
@@ -987,14 +995,15 @@ const KernelVariant &variant(bool /*small: the A/B harness picks by index*/ = fa
 // choice only changes speed.  (One kernel holding both loops
 // needs more than the 80 VGPRs six waves per SIMD allow: 40 B/lane of
 // scratch.)
-const KernelVariant kDefault = {"v3_wg768_nt_dyn4c4p32_sp",
-                                crc_batch_kernel_v3<768, 6, false, 0, UNIT_OVH, false, true, false, 0, 4, 4, 32, true>,
+const KernelVariant kDefault = {"v3_wg768_nt_dyn4c4p32_sp_xp",
+                                crc_batch_kernel_v3<768, 6, false, 0, UNIT_OVH, false, true, false, 0, 4, 4, 32, true,
+                                                    0, false, false, true>,
                                 768};
 // (its records are below DWG_MIN_BYTES, so it is built without the dword
 // grid's code: BMG)
-const KernelVariant kSmall = {"v3_wg768_nt_dyn4c4p32_sp_pp_wait_bmg",
+const KernelVariant kSmall = {"v3_wg768_nt_dyn4c4p32_sp_pp_wait_bmg_xp",
                               crc_batch_kernel_v3<768, 6, false, 0, UNIT_OVH, false, true, false, 0, 4, 4, 32, true, 3,
-                                                  false, true>,
+                                                  false, true, true>,
                               768};
 const KernelVariant &variant(bool small = false) { return small ? kSmall : kDefault; }
 #endif
