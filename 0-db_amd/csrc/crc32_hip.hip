@@ -708,8 +708,12 @@ __global__ __launch_bounds__(WGT, WPE) void crc_batch_kernel_v3(
     uint64_t pbase = 0; // units of earlier ranges (PRIO progress)
     // tail pool of this workgroup: chunk c covers [P0 + PL c / nch, P0 + PL (c+1) / nch)
     // XP: the workgroups of a pool come from every XCD (workgroup b runs on XCD
-    // b mod 8), so that a slower XCD's share of the pool is taken by the others
-    const uint32_t pool = (XP ? blockIdx.x >> 3 : blockIdx.x) % DYN_POOLS;
+    // b mod 8), so that a slower XCD's share of the pool is taken by the
+    // others: each run of DYN_POOLS consecutive workgroups covers every pool
+    // once (so any grid of >= DYN_POOLS workgroups serves every pool, as the
+    // guard above requires), rotated by one per run (pool p gets XCDs p,
+    // p - 1, ..., p - 15 mod 8 of a 512-workgroup grid: each twice)
+    const uint32_t pool = (XP ? blockIdx.x + blockIdx.x / DYN_POOLS : blockIdx.x) % DYN_POOLS;
     const uint64_t Td = total - Ts;
     const uint64_t P0 = Ts + Td * pool / DYN_POOLS;
     const uint64_t PL = Ts + Td * (pool + 1) / DYN_POOLS - P0;
