@@ -89,6 +89,26 @@ def test_device_walk_many_files_one_image(dev):
     assert walked(st, len(allw)) == allw
 
 
+def test_device_walk_more_files_than_one_stitch_block(dev):
+    """300 files (the stitch kernel folds the file prefix into its one block
+    up to 256 files; beyond that the prefix is a kernel of its own): every
+    golden file repeated, record offsets, per-file status and totals"""
+    names = (CASES * 28)[:300]
+    imgs = [np.fromfile(GOLDEN / "datafiles" / f"{n}.d0", dtype=np.uint8) for n in names]
+    st, offs = store(dev, imgs)
+    st.walk(65536)
+    torch.cuda.synchronize()
+    rec, status, rew = file_results(st)
+    allw = []
+    for i, im in enumerate(imgs):
+        w, s = serial(im)
+        assert int(status[i]) == s, names[i]
+        assert int(rec[i]) == len(allw)
+        allw += [(a + offs[i], b + offs[i], c, d) for a, b, c, d in w]
+    assert int(rec[len(imgs)]) == len(allw)
+    assert walked(st, len(allw)) == allw
+
+
 def test_device_walk_broken_previous_chain(dev):
     img = np.fromfile(GOLDEN / "datafiles" / "zipf_small.d0", dtype=np.uint8).copy()
     recs, _ = dev.datafile_walk(img)
