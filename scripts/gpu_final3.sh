@@ -9,5 +9,5 @@ timeout -k 10 600 python -u -m pytest tests -x -q -m gpu --timeout 120 --timeout
 timeout -k 10 400 python bench.py > gpurun_out/$T/bench.json 2> gpurun_out/$T/bench.err && \
 timeout -k 10 400 python bench.py --gpus 2 --steps 5 --warmup 2 > gpurun_out/$T/bench_n2.json 2> gpurun_out/$T/bench_n2.err && \
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/$T/trace -o run -- \
-    python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline > gpurun_out/$T/trace_bench.json 2> gpurun_out/$T/trace_bench.err && \
+    python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-extra > gpurun_out/$T/trace_bench.json 2> gpurun_out/$T/trace_bench.err && \
 python3 scripts/trace_summary.py gpurun_out/$T/trace/run_kernel_trace.csv 20 > gpurun_out/$T/trace_summary.json
