@@ -965,6 +965,10 @@ const KernelVariant kVariants[] = {
     {"v3_wg768_nt_dyn4c4p32_sp", crc_batch_kernel_v3<768, 6, false, 0, UNIT_OVH, false, true, false, 0, 4, 4, 32, true>, 768},
     {"v3_wg768_nt_dyn4c4p32_sp_pp_wait_bmg_xp", crc_batch_kernel_v3<768, 6, false, 0, UNIT_OVH, false, true, false, 0, 4, 4, 32, true, 3, false, true, true>, 768},
     {"v3_wg768_nt_dyn4c4p32_sp_stamp_xp", crc_batch_kernel_v3<768, 6, true, 0, UNIT_OVH, false, true, false, 0, 4, 4, 32, true, 0, false, false, true>, 768},
+    // round 2: pool share and chunks per wave re-checked with the XCD pools
+    {"v3_wg768_nt_dyn3c4p32_sp_xp", crc_batch_kernel_v3<768, 6, false, 0, UNIT_OVH, false, true, false, 0, 3, 4, 32, true, 0, false, false, true>, 768},
+    {"v3_wg768_nt_dyn5c4p32_sp_xp", crc_batch_kernel_v3<768, 6, false, 0, UNIT_OVH, false, true, false, 0, 5, 4, 32, true, 0, false, false, true>, 768},
+    {"v3_wg768_nt_dyn4c3p32_sp_xp", crc_batch_kernel_v3<768, 6, false, 0, UNIT_OVH, false, true, false, 0, 4, 3, 32, true, 0, false, false, true>, 768},
     // round 2, after the dword grid: planning charge and pool share re-checked
     {"v3_wg768_nt_dyn4c4p32_sp_uo256", crc_batch_kernel_v3<768, 6, false, 0, 256, false, true, false, 0, 4, 4, 32, true>, 768, WG_PER_CU, 256},
     {"v3_wg768_nt_dyn4c4p32_sp_uo512", crc_batch_kernel_v3<768, 6, false, 0, 512, false, true, false, 0, 4, 4, 32, true>, 768, WG_PER_CU, 512},
