@@ -373,6 +373,7 @@ struct PlanArgs {
     uint32_t nb;
     uint32_t lg;
     const uint32_t *bmax; // nb block maxima of a record's unit count (tail-pool guard)
+    const uint64_t *dn;   // nullptr, or the record count in device memory (n is then its bound)
 };
 
 __device__ __forceinline__ uint32_t wave_max(uint32_t x) {
@@ -597,6 +598,10 @@ __global__ __launch_bounds__(WGT, WPE) void crc_batch_kernel_v3(
     uint32_t *__restrict__ out, const uint32_t *__restrict__ tables, uint32_t max_waves,
     uint32_t *__restrict__ scratch, uint32_t epoch) {
     constexpr uint32_t NW = WGT / 64, NSLOT = 2 * NW;
+    if (plan.dn) { // the record count left in device memory by the producer (f3 walk): n is its bound
+        const uint64_t dn = *plan.dn;
+        n = dn < n ? dn : n;
+    }
     __shared__ __attribute__((aligned(16))) uint32_t lds[ZDBCRC_LDS_DW + 16 + 2 * NSLOT];
     __shared__ uint64_t boff[PLAN_MAX_BLOCKS + 1];
     __shared__ uint64_t wsum[2 * NW + 1];
@@ -1047,7 +1052,11 @@ __global__ __launch_bounds__(PLAN_T) void plan_kernel(const uint8_t *__restrict_
                                                       const uint32_t *__restrict__ lengths, uint64_t n, uint64_t ovh,
                                                       uint32_t lg, uint64_t *__restrict__ local,
                                                       uint64_t *__restrict__ bsum, uint32_t *__restrict__ bmax,
-                                                      uint32_t *__restrict__ out) {
+                                                      uint32_t *__restrict__ out, const uint64_t *__restrict__ dn) {
+    if (dn) { // device-side record count, n its bound (records past it: no units)
+        const uint64_t m = *dn;
+        n = m < n ? m : n;
+    }
     __shared__ uint64_t wsum[2 * (PLAN_T / 64) + 1];
     __shared__ uint32_t wmx[PLAN_T / 64];
     uint32_t mx = 0;
@@ -1099,7 +1108,11 @@ __global__ __launch_bounds__(PLAN_T) void plan_kernel(const uint8_t *__restrict_
 
 __global__ void verify_kernel(const uint32_t *__restrict__ out, const uint32_t *__restrict__ expected,
                               uint64_t n, uint32_t *__restrict__ mismatch, uint32_t *__restrict__ count,
-                              uint32_t max_mismatch) {
+                              uint32_t max_mismatch, const uint64_t *__restrict__ dn) {
+    if (dn) {
+        const uint64_t m = *dn;
+        n = m < n ? m : n;
+    }
     const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (r < n && out[r] != expected[r]) {
         const uint32_t idx = atomicAdd(count, 1u);
@@ -1386,7 +1399,8 @@ int ensure_device(int dev, DeviceCtx **out_ctx) {
 // out_zeroed: a host-planned batch whose out[] is already zero (latency path)
 int enqueue_batch(int dev, DeviceCtx &c, const KernelVariant &kv, const uint8_t *arena, const uint64_t *offsets,
                   const uint32_t *lengths, uint32_t *out, uint64_t n, hipStream_t st,
-                  const uint64_t *d_unit_start = nullptr, uint32_t grid_wgs = 0, bool out_zeroed = false) {
+                  const uint64_t *d_unit_start = nullptr, uint32_t grid_wgs = 0, bool out_zeroed = false,
+                  const uint64_t *d_n = nullptr) {
     if (n > 0xFFFFFFFFull) // record indices are 32-bit on the device (cut lists, mismatch indices)
         return ZDB_CRC32_EINVAL;
     // planner blocks: 2^lg records each (n + 1 entries), at most PLAN_MAX_BLOCKS
@@ -1420,17 +1434,17 @@ int enqueue_batch(int dev, DeviceCtx &c, const KernelVariant &kv, const uint8_t 
 #ifdef ZDBCRC_DIAG
     g_last_scratch = scratch;
 #endif
-    PlanArgs plan{d_unit_start, nullptr, 0, 0, nullptr};
+    PlanArgs plan{d_unit_start, nullptr, 0, 0, nullptr, d_n};
     if (!d_unit_start) {
         uint8_t *base = static_cast<uint8_t *>(w.ptr) + scratch_bytes;
         uint64_t *local = reinterpret_cast<uint64_t *>(base);
         uint64_t *bsum = reinterpret_cast<uint64_t *>(base + local_bytes);
         uint32_t *bmax = reinterpret_cast<uint32_t *>(base + local_bytes + bsum_bytes);
         hipLaunchKernelGGL(plan_kernel, dim3((uint32_t)nb), dim3(PLAN_T), 0, st, arena, offsets, lengths, n,
-                           (uint64_t)kv.unit_ovh, lg, local, bsum, bmax, out);
+                           (uint64_t)kv.unit_ovh, lg, local, bsum, bmax, out, d_n);
         if (hipGetLastError() != hipSuccess)
             return ZDB_CRC32_ELAUNCH;
-        plan = PlanArgs{local, bsum, (uint32_t)nb, lg, bmax};
+        plan = PlanArgs{local, bsum, (uint32_t)nb, lg, bmax, d_n};
     } else if (!out_zeroed && hipMemsetAsync(out, 0, n * sizeof(uint32_t), st) != hipSuccess) {
         return ZDB_CRC32_ELAUNCH;
     }
@@ -1703,9 +1717,13 @@ int zdb_crc32_batch_device_sized(const uint8_t *d_arena, const uint64_t *d_offse
                          static_cast<hipStream_t>(stream));
 }
 
-int zdb_crc32_verify_device(const uint8_t *d_arena, const uint64_t *d_offsets, const uint32_t *d_lengths,
-                            const uint32_t *d_expected, uint32_t *d_out, uint32_t *d_mismatch,
-                            uint32_t *d_mismatch_count, uint32_t max_mismatch, size_t n, void *stream) {
+// zdb_crc32_verify_device with, optionally, the record count in device
+// memory (d_n; n is then its bound): the f3 scan verifies what its walk
+// found without a host round trip for the count (not exported)
+int zdbcrc_internal_verify_device_dn(const uint8_t *d_arena, const uint64_t *d_offsets, const uint32_t *d_lengths,
+                                     const uint32_t *d_expected, uint32_t *d_out, uint32_t *d_mismatch,
+                                     uint32_t *d_mismatch_count, uint32_t max_mismatch, size_t n,
+                                     const uint64_t *d_n, void *stream) {
     if (!d_mismatch_count || !d_expected || (max_mismatch && !d_mismatch))
         return ZDB_CRC32_EINVAL;
     hipStream_t st = static_cast<hipStream_t>(stream);
@@ -1724,14 +1742,21 @@ int zdb_crc32_verify_device(const uint8_t *d_arena, const uint64_t *d_offsets, c
             return ZDB_CRC32_OK;
         if (!d_arena || !d_offsets || !d_lengths || !d_out)
             return ZDB_CRC32_EINVAL;
-        rc = enqueue_batch(dev, *c, variant(), d_arena, d_offsets, d_lengths, d_out, n, st);
+        rc = enqueue_batch(dev, *c, variant(), d_arena, d_offsets, d_lengths, d_out, n, st, nullptr, 0, false, d_n);
         if (rc)
             return rc;
     }
     const uint32_t blocks = (uint32_t)((n + 255) / 256);
     hipLaunchKernelGGL(verify_kernel, dim3(blocks), dim3(256), 0, st, d_out, d_expected, (uint64_t)n,
-                       d_mismatch, d_mismatch_count, max_mismatch);
+                       d_mismatch, d_mismatch_count, max_mismatch, d_n);
     return hipGetLastError() == hipSuccess ? ZDB_CRC32_OK : ZDB_CRC32_ELAUNCH;
+}
+
+int zdb_crc32_verify_device(const uint8_t *d_arena, const uint64_t *d_offsets, const uint32_t *d_lengths,
+                            const uint32_t *d_expected, uint32_t *d_out, uint32_t *d_mismatch,
+                            uint32_t *d_mismatch_count, uint32_t max_mismatch, size_t n, void *stream) {
+    return zdbcrc_internal_verify_device_dn(d_arena, d_offsets, d_lengths, d_expected, d_out, d_mismatch,
+                                            d_mismatch_count, max_mismatch, n, nullptr, stream);
 }
 
 int zdb_datafile_check_device(const uint8_t *d_image, uint64_t image_len, const uint64_t *d_offsets,

@@ -54,6 +54,9 @@
 #include "zdb_datafile.h"
 
 extern "C" void zdbcrc_internal_mark_hip(void); // crc32_hip.hip (not exported)
+extern "C" int zdbcrc_internal_verify_device_dn(const uint8_t *, const uint64_t *, const uint32_t *, const uint32_t *,
+                                                uint32_t *, uint32_t *, uint32_t *, uint32_t, size_t,
+                                                const uint64_t *, void *); // crc32_hip.hip (not exported)
 
 namespace {
 
@@ -1006,17 +1009,26 @@ int zdb_datafile_scan_device(const uint8_t *d_image, const uint64_t *d_file_off,
     if (rc)
         return rc;
     hipStream_t st = static_cast<hipStream_t>(stream);
+    if (!nfiles || !b->capacity)
+        return zdb_crc32_verify_device(d_image, b->payload_off, b->payload_len, b->expected, b->computed,
+                                       b->mismatch, b->mismatch_count, b->max_mismatch, 0, stream);
+    // the verify reads the walk's record count from device memory (bounded by
+    // the capacity: a walk that found more records wrote only that many), so
+    // no host round trip separates the two; the count comes back at the end
+    const uint64_t bound = b->capacity < 0xFFFFFFFFull ? b->capacity : 0xFFFFFFFFull; // 32-bit record indices
+    rc = zdbcrc_internal_verify_device_dn(d_image, b->payload_off, b->payload_len, b->expected, b->computed,
+                                          b->mismatch, b->mismatch_count, b->max_mismatch, bound,
+                                          b->file_records + nfiles, stream);
+    if (rc)
+        return rc;
     uint64_t n = 0;
-    if (nfiles) {
-        if (hipMemcpyAsync(&n, b->file_records + nfiles, sizeof(n), hipMemcpyDeviceToHost, st) != hipSuccess ||
-            hipStreamSynchronize(st) != hipSuccess)
-            return ZDB_CRC32_ELAUNCH;
-    }
+    if (hipMemcpyAsync(&n, b->file_records + nfiles, sizeof(n), hipMemcpyDeviceToHost, st) != hipSuccess ||
+        hipStreamSynchronize(st) != hipSuccess)
+        return ZDB_CRC32_ELAUNCH;
     *n_records = n;
     if (n > b->capacity)
         return ZDB_CRC32_ENOSPC;
-    return zdb_crc32_verify_device(d_image, b->payload_off, b->payload_len, b->expected, b->computed,
-                                   b->mismatch, b->mismatch_count, b->max_mismatch, n, stream);
+    return n > bound ? ZDB_CRC32_EINVAL : ZDB_CRC32_OK; // more records than 32-bit indices reach
 }
 
 } // extern "C"

@@ -141,10 +141,12 @@ typedef struct zdb_scan_buffers_t {
 } zdb_scan_buffers_t;
 
 /* The integrity scan of a whole store, device-resident (tools/integrity-check
- * over every file: integrity-check.c:59-105): zdb_datafile_walk_device, one
- * synchronisation to learn the record count (*n_records), then the batched
- * checksum + compare (zdb_crc32_verify_device) over the walked records.
- * Returns ZDB_CRC32_ENOSPC (with *n_records set) when capacity is too small. */
+ * over every file: integrity-check.c:59-105): zdb_datafile_walk_device, then
+ * the batched checksum + compare (zdb_crc32_verify_device) over the walked
+ * records -- the record count stays in device memory between the two -- and
+ * one synchronisation at the end that returns it (*n_records).
+ * Returns ZDB_CRC32_ENOSPC (with *n_records set; computed / mismatch then
+ * cover the first `capacity` records only) when capacity is too small. */
 int zdb_datafile_scan_device(const uint8_t *d_image, const uint64_t *d_file_off, const uint64_t *d_file_len,
                              uint32_t nfiles, uint64_t max_file_len, uint32_t chunk_bytes,
                              const zdb_scan_buffers_t *buffers, uint64_t *n_records, void *stream);

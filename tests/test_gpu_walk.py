@@ -150,6 +150,10 @@ def test_device_walk_bound_and_capacity(dev):
     small, _ = store(dev, [img], capacity=5)
     with pytest.raises(dev.ZdbCrcError, match="capacity"):
         small.scan(2048)
+    # the verify ran on the device-side count bounded by the capacity: the
+    # first 5 records are checked (mixed.d0 is clean: computed == stored)
+    want, _ = serial(img)
+    assert small.computed[:5].cpu().numpy().view(np.uint32).tolist() == [w[3] for w in want[:5]]
     assert dev._walk_device(None, None, None, 1, 1, 0, None, None, None, None, 0, None, None, None, None) == -2
 
 
