@@ -190,9 +190,9 @@ def c4_leg(rank: int, world: int, steps: int, warmup: int, settle_s: float, barr
     """the integrity scan of this rank's 64 reference-valid
     datafiles (~16 GiB), device-resident, from the images alone: one step =
     zdb_datafile_scan_device = the GPU record-boundary discovery (f3: chunked
-    speculative walk + exact stitch), one synchronisation for the record
-    count, then plan + checksum + compare with the `integrity` field of every
-    entry header.  The image is built in HBM (synthetic bytes, then the
+    speculative walk + exact stitch), then plan + checksum + compare with the
+    `integrity` field of every entry header over the record count the walk
+    left in device memory, and one synchronisation at the end.  The image is built in HBM (synthetic bytes, then the
     headers, whose crcs come from an untimed checksum pass and are checked
     against the reference's digest of this shard).  Reported beside it: the
     walk alone and the verify with descriptors known in advance (round 1's
