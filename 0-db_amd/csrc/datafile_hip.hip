@@ -877,7 +877,10 @@ int zdb_datafile_walk_device(const uint8_t *d_image, const uint64_t *d_file_off,
         return ZDB_CRC32_EINVAL;
     const uint64_t cpf64 = max_file_len ? (max_file_len + (1ull << lg) - 1) >> lg : 1;
     const uint64_t nchunks = cpf64 * nfiles;
-    if (nchunks > (1ull << 31))
+    // one search workgroup of SEARCH_T threads per chunk and up to 512 slot
+    // threads per chunk in the copy: keep every grid below 2^32 threads, so
+    // an oversized store fails here and not as a late launch error
+    if (nchunks >= (1ull << 32) / SEARCH_T || nchunks * (nchunks <= 65536 ? 512u : 64u) >= (1ull << 32))
         return ZDB_CRC32_EINVAL;
     zdbcrc_internal_mark_hip();
     int dev = 0;
@@ -1009,7 +1012,17 @@ int zdb_datafile_scan_device(const uint8_t *d_image, const uint64_t *d_file_off,
     if (rc)
         return rc;
     hipStream_t st = static_cast<hipStream_t>(stream);
-    if (!nfiles || !b->capacity)
+    if (nfiles && !b->capacity) {
+        // a size query: the walk ran and counted; nothing was checksummed
+        uint64_t n = 0;
+        if (hipMemsetAsync(b->mismatch_count, 0, sizeof(uint32_t), st) != hipSuccess ||
+            hipMemcpyAsync(&n, b->file_records + nfiles, sizeof(n), hipMemcpyDeviceToHost, st) != hipSuccess ||
+            hipStreamSynchronize(st) != hipSuccess)
+            return ZDB_CRC32_ELAUNCH;
+        *n_records = n;
+        return n ? ZDB_CRC32_ENOSPC : ZDB_CRC32_OK;
+    }
+    if (!nfiles)
         return zdb_crc32_verify_device(d_image, b->payload_off, b->payload_len, b->expected, b->computed,
                                        b->mismatch, b->mismatch_count, b->max_mismatch, 0, stream);
     // the verify reads the walk's record count from device memory (bounded by

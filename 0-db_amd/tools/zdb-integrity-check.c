@@ -358,6 +358,9 @@ typedef struct {
     int gpus;          /* devices to spread the workers over (0 = all)        */
     int stale_errno;   /* errno a fresh process has after its first localtime */
     int trace;         /* ZDBCRC_TOOL_TRACE: per-file phase times on stderr   */
+    int auto_wait;     /* ZDBCRC_AUTO_START_GPU=1 (tests): auto waits for the
+                          GPU start-up instead of taking the scalar engine for
+                          files whose checksum starts before it is up        */
 } config_t;
 
 typedef struct {
@@ -570,7 +573,7 @@ static void check_file(const config_t *cfg, worker_t *w, const char *filename, r
             }
             use_gpu = 1;
         } else if (cfg->engine == ENGINE_AUTO) {
-            use_gpu = !gpu_failed && (streaming || gpu_state(0) == 1);
+            use_gpu = !gpu_failed && (streaming || gpu_state(cfg->auto_wait) == 1);
         }
         if (use_gpu) {
             int rc = 0;
@@ -599,6 +602,8 @@ static void check_file(const config_t *cfg, worker_t *w, const char *filename, r
         }
     }
     const double t_fmt = now_s();
+    if (cfg->trace && m)
+        fprintf(stderr, "[trace] %s: checksum engine %s, %zu payloads\n", filename, engine_used, m);
 
     outbuf_t *ob = &r->out;
     size_t k = 0;
@@ -712,7 +717,7 @@ static void usage(const char *prog) {
 }
 
 int main(int argc, char *argv[]) {
-    config_t cfg = {ENGINE_AUTO, 0, 0, getenv("ZDBCRC_TOOL_TRACE") != NULL};
+    config_t cfg = {ENGINE_AUTO, 0, 0, getenv("ZDBCRC_TOOL_TRACE") != NULL, 0};
     int jobs = 0;
     int argi = 1;
     while (argi < argc && strncmp(argv[argi], "--", 2) == 0) {
@@ -747,7 +752,8 @@ int main(int argc, char *argv[]) {
     if (njobs > argc - argi)
         njobs = argc - argi;
     const char *force_gpu = getenv("ZDBCRC_AUTO_START_GPU"); /* tests: start the GPU whatever the size */
-    if (cfg.engine == ENGINE_AUTO && !(force_gpu && force_gpu[0] == '1')) {
+    cfg.auto_wait = force_gpu && force_gpu[0] == '1';
+    if (cfg.engine == ENGINE_AUTO && !cfg.auto_wait) {
         double gib = 0;
         for (int i = argi; i < argc; i++) {
             struct stat fst;

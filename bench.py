@@ -291,6 +291,20 @@ def cpu_baseline(offs, lens, seed, seconds: float) -> dict | None:
         if time.perf_counter() - t0 >= seconds:
             break
     mt = passes * total / (time.perf_counter() - t0) / GIB
+    # SURVEY §8(d) also asks for the host's whole CPU count: every CPU of the
+    # affinity mask (on the GPU box many of them belong to other jobs' shares,
+    # so this is an upper bound that the job share above does not claim)
+    full = len(os.sched_getaffinity(0))
+    full_res = None
+    if kind == "reference" and full > threads:
+        fp, t0 = 0, time.perf_counter()
+        while True:
+            run(full)
+            fp += 1
+            if time.perf_counter() - t0 >= seconds:
+                break
+        full_res = {"value": round(fp * total / (time.perf_counter() - t0) / GIB, 3), "unit": "GiB/s",
+                    "cores": full, "passes": fp}
     n1 = int(np.searchsorted(np.cumsum(lens), 1 << 30)) + 1  # ~1 GiB prefix
     t0 = time.perf_counter()
     if kind == "reference":
@@ -304,8 +318,9 @@ def cpu_baseline(offs, lens, seed, seconds: float) -> dict | None:
                       f"threads ({seconds:.0f}+ s wall); single-thread {st:.2f} GiB/s on a "
                       f"{b1 >> 20} MiB prefix",
             "single_thread_gibs": round(st, 3), "cpu_model": cpu_model(),
-            "affinity_cpus": len(os.sched_getaffinity(0)),
-            "threads_rule": "one thread per CPU of this job's share: min(sched_getaffinity, OMP_NUM_THREADS)"}
+            "affinity_cpus": full, "all_affinity_cpus": full_res,
+            "threads_rule": "value: one thread per CPU of this job's share, min(sched_getaffinity, "
+                            "OMP_NUM_THREADS); all_affinity_cpus: one thread per CPU of the affinity mask"}
 
 
 def cpu_threads() -> int:
@@ -542,15 +557,19 @@ def combine_ranks(elapsed_s: float, payload: int, world: int) -> tuple[float, fl
     return float(t.item()), float(b.item())
 
 
-def pmc_traffic(workload: str):
+def pmc_traffic(workload: str) -> tuple:
+    """(HBM bytes per launch, where that number was measured): the PMC pass
+    cannot run inside this process (rocprofv3 wraps the whole program), so
+    the figure is the committed FETCH_SIZE pass of the same kernel
+    (profiles/pmc_traffic.json), labelled with its source"""
     p = ROOT / "profiles" / "pmc_traffic.json"
     if not p.exists():
-        return None
+        return None, None
     try:
-        d = json.loads(p.read_text())
-        return d.get(workload, {}).get("hbm_bytes_per_launch")
+        d = json.loads(p.read_text()).get(workload, {})
+        return d.get("hbm_bytes_per_launch"), d.get("source")
     except Exception:
-        return None
+        return None, None
 
 
 def shard_digest_ref(kind: str, rank: int, gib: float) -> dict | None:
@@ -567,6 +586,19 @@ def shard_digest_ref(kind: str, rank: int, gib: float) -> dict | None:
     if rank == 0 and kind in d and gib == 4.0:  # round-1 layout: rank 0 only
         return d[kind]
     return None
+
+
+def workload_parity(workload: str, out, rank: int, gib: float) -> str:
+    """the full-size output of one workload (the device `out` tensor of the
+    last step) against the reference's digest of it: C3 per rank, C2 and
+    C2u for rank 0's 4 GiB batch (tests/golden/digests.json)"""
+    got = digest(out.cpu().numpy().view(np.uint32))
+    if workload == "zipf":
+        return parity_of(got, shard_digest_ref("C3", rank, gib), f"C3 shard {rank}")
+    key = {"fixed4k": "C2", "c2u": "C2u"}[workload]
+    if rank == 0 and gib == 4.0:
+        return parity_of(got, json.loads((ROOT / "tests/golden/digests.json").read_text()).get(key), key)
+    return "unchecked (no reference digest for this shard)"
 
 
 def parity_of(got: dict, ref: dict | None, what: str) -> str:
@@ -707,6 +739,8 @@ def main():
     ap.add_argument("--no-c4", action="store_true", help="skip the C4 integrity-scan leg")
     ap.add_argument("--settle-s", type=float, default=1.0,
                     help="untimed steps after the warmup until this many seconds have passed")
+    ap.add_argument("--rehearsal", action="store_true",
+                    help="allow more ranks than visible GPUs (ranks share devices over gloo; the line says so)")
     ap.add_argument("--device", default="gpu", choices=["gpu", "cpu"],
                     help="cpu: multi-rank plumbing test on gloo with the scalar engine (tests only)")
     args = ap.parse_args()
@@ -733,6 +767,12 @@ def main():
     # GPUs -- a rehearsal of the N-rank plumbing on a one-GPU box -- share the
     # devices round-robin and use gloo, which allows that.
     ndev = torch.cuda.device_count()
+    shared = world > ndev
+    if shared and not args.rehearsal:
+        # a --gpus N line from fewer than N devices would read as an N-GPU
+        # weak-scaling result; only an explicit rehearsal may share devices
+        sys.exit(f"bench.py: {world} ranks but {ndev} visible GPU(s): refusing to report a {world}-GPU result "
+                 "(pass --rehearsal to run the N-rank plumbing on shared devices; the line is then marked)")
     local = local % max(ndev, 1)
     torch.cuda.set_device(local)
     # stdout carries exactly one JSON line: the communication libraries print
@@ -774,13 +814,7 @@ def main():
     # parity at full size: every rank's shard against the reference's digest of it
     step()
     torch.cuda.synchronize()
-    got = digest(out.cpu().numpy().view(np.uint32))
-    if args.workload == "zipf":
-        parity = parity_of(got, shard_digest_ref("C3", rank, args.gib), f"C3 shard {rank}")
-    elif args.workload == "fixed4k" and rank == 0 and args.gib == 4.0:
-        parity = parity_of(got, json.loads((ROOT / "tests/golden/digests.json").read_text()).get("C2"), "C2")
-    else:
-        parity = "unchecked (no reference digest for this shard)"
+    parity = workload_parity(args.workload, out, rank, args.gib)
     log(f"rank {rank} parity: {parity}")
     for _ in range(args.warmup):
         step()
@@ -813,8 +847,10 @@ def main():
     avg_kernel_s = kern_ms / max(launches, 1) / 1e3
     alg_bytes = payload + 16 * n  # len + 8 B offset + 4 B length + 4 B crc
     achieved = alg_bytes / avg_kernel_s / 1e9
+    traffic, traffic_src = pmc_traffic(args.workload)
     roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": pmc_traffic(args.workload),
+                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                "traffic_source": f"rocprofv3 --pmc FETCH_SIZE pass (separate run): {traffic_src}" if traffic else None,
                 "kernel": "crc_batch_kernel", "avg_kernel_ms": round(avg_kernel_s * 1e3, 4),
                 "alg_bytes_per_launch": alg_bytes}
 
@@ -853,8 +889,12 @@ def main():
             zdbcrc.set_timing(False)
             km, kl = zdbcrc.kernel_stats()
             pb = int(l2.sum())
+            # the output of the last timed step, at full size, against the reference
+            p2 = workload_parity(other, out2, 0, args.gib)
+            log(f"{other} parity: {p2}")
             extra[other] = {"desc": d2, "records": len(l2), "gibs": round(pb * args.steps / (tb - ta) / GIB, 2),
-                            "kernel_ms": round(km / max(kl, 1), 4),
+                            "shape": "small-record (max_length 4096)" if ml else "default",
+                            "parity": p2, "kernel_ms": round(km / max(kl, 1), 4),
                             "roofline_frac": round((pb + 16 * len(l2)) / (km / max(kl, 1) / 1e3) / 1e9
                                                    / HBM_PEAK_GBS, 4)}
             del a2, do2, dl2, out2
@@ -875,6 +915,7 @@ def main():
     if rank == 0:
         line = {
             "metric": METRIC, "value": round(value, 2), "unit": "GiB/s", "n_gpus": world,
+            "physical_gpus": ndev, "shared_devices": shared,
             "steps": args.steps, "warmup": args.warmup, "settle_steps": settle,
             "ms_per_step": round(ms_per_step, 4),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",

@@ -56,6 +56,15 @@ for wl in [w for w in work.split(",") if w and w != "none"]:
         lens = zdbcrc.zipf_lengths(size, 0xC3C3C3).astype(np.int64)
         seed = 0x5A0DB5EED + 3
         align = 16 if wl == "zipf16" else 1
+    elif wl in ("zipf_small", "zipf_large"):
+        # C3's records split by size (<= 4 KiB / larger), each class tiled
+        # until the batch holds `size` bytes: per-record vs per-byte cost
+        base = zdbcrc.zipf_lengths(4 << 30, 0xC3C3C3).astype(np.int64)
+        base = base[base <= 4096] if wl == "zipf_small" else base[base > 4096]
+        reps = max(1, -(-size // int(base.sum())))
+        lens = np.tile(base, reps)
+        lens = lens[:int(np.searchsorted(np.cumsum(lens), size))]
+        seed = 0x5A0DB5EED + 3
     elif wl == "single":
         lens = np.array([size - 16], np.int64); seed = 0x5A0DB5EED
     elif wl == "fixed64k":

@@ -193,6 +193,7 @@ def digests(ref: oracle.Reference) -> dict:
     out["C3"] = {"seed": C3_SEED, "len_seed": C3_LEN_SEED, "target": 4 << 30, "total_bytes": total,
                  **digest(ref, c3)}
     del arena
+    out["C2u"] = c2u_digest(ref)
     out["C4"] = digest_c4(ref)
     out["MAX"] = max_digest(ref)
     return out
@@ -260,6 +261,21 @@ def c4_shard_digest(ref: oracle.Reference, rank: int) -> dict:
             "payload_bytes": int(lay["lens"].sum()), **digest(ref, c4)}
 
 
+def c2u_digest(ref: oracle.Reference) -> dict:
+    """bench.make_dataset("c2u", 4 GiB, 0): the C2 payload count (1 Mi x 4 KiB)
+    laid out as a datafile image, payload i at 28 + i * 4122 + 26 (SURVEY
+    §8(d) C2u), bytes from splitmix64(C2_SEED) over the whole image"""
+    import zdbcrc
+    sys.path.insert(0, str(ROOT))
+    import bench
+    offs, lens, seed, _ = bench.make_dataset("c2u", 4 << 30, 0)
+    total = int(offs[-1] + lens[-1])
+    arena = zdbcrc.synth_fill(total, seed)
+    crcs = ref.batch(arena, offs.astype(np.uint64), lens.astype(np.uint32), threads=8)
+    return {"seed": seed, "records": len(lens), "record_bytes": 4096, "first_offset": int(offs[0]),
+            "stride": int(offs[1] - offs[0]), "total_bytes": total, **digest(ref, crcs)}
+
+
 def rank_digests(ref: oracle.Reference, ranks: int = 8) -> dict:
     """every rank's shard of a multi-GPU bench run (bench.py --gpus N, N <= 8):
     the full-size C3 (4 GiB) and C4 (64 datafiles) shards, and the 16 MiB C3
@@ -287,6 +303,12 @@ def main():
         d["MAX"] = max_digest(ref)
         (OUT / "digests.json").write_text(json.dumps(d, indent=1) + "\n")
         print("digests.json MAX:", d["MAX"])
+        return
+    if "--only-c2u" in sys.argv:  # add / refresh the C2u digest only
+        d = json.loads((OUT / "digests.json").read_text())
+        d["C2u"] = c2u_digest(ref)
+        (OUT / "digests.json").write_text(json.dumps(d, indent=1) + "\n")
+        print("digests.json C2u:", d["C2u"])
         return
     if "--only-c4" in sys.argv:  # add / refresh the C4 digest only
         d = json.loads((OUT / "digests.json").read_text())

@@ -239,6 +239,32 @@ def test_full_size_c2_digest(dev, oracle_c, digests):
     del arena
 
 
+@pytest.mark.parametrize("workload", ["fixed4k", "c2u"])
+@pytest.mark.parametrize("max_length", [None, 4096])
+def test_full_size_small_record_digests(dev, oracle_c, digests, workload, max_length):
+    """C2 (4 KiB-aligned) and C2u (4 KiB payloads behind 26-byte datafile
+    headers, byte-misaligned: SURVEY §8(d)) at full size, 1 Mi records each,
+    in BOTH loop shapes the library carries -- the default and the
+    small-record shape that zdb_crc32_batch_device_sized picks for
+    max_length <= 4096, i.e. the shape bench.py times for these workloads --
+    bit-exact vs the reference's digest (make_golden.py --only-c2u)."""
+    sys.path.insert(0, str(ROOT))
+    import bench
+    d = digests["C2" if workload == "fixed4k" else "C2u"]
+    offs, lens, seed, _ = bench.make_dataset(workload, 4 << 30, 0)
+    assert seed == d["seed"] and len(lens) == d["count"]
+    total = int(offs[-1] + lens[-1])
+    arena = torch.empty(total + 64, dtype=torch.uint8, device="cuda")
+    dev.synth_fill_device(arena[:total], seed)
+    out = torch.empty(len(lens), dtype=torch.int32, device="cuda")
+    dev.batch_device(arena, torch.from_numpy(offs).cuda(), torch.from_numpy(lens.astype(np.int32)).cuda(), out,
+                     max_length=max_length)
+    torch.cuda.synchronize()
+    got = _digest(oracle_c.crc32, out.cpu().numpy().view(np.uint32))
+    assert got == {k: d[k] for k in ("count", "xor", "crc_of_crcs")}
+    del arena
+
+
 def test_full_size_c3_digest(dev, oracle_c, digests):
     """C3 at BASELINE size (Zipf 64 B..1 MiB, ~4 GiB, any alignment)."""
     d = digests["C3"]
@@ -323,16 +349,34 @@ TOOL_CASES = ["mixed", "zipf_small", "fixed_4k", "corrupt_payload", "corrupt_crc
               "truncated_payload", "truncated_header", "bad_magic", "bad_version", "header_only"]
 
 
+NO_PAYLOAD_CASES = {"bad_magic", "bad_version", "header_only"}  # the tool never reaches a checksum
+
+
+def split_trace(err):
+    """(stderr without the ZDBCRC_TOOL_TRACE lines, the checksum engines those lines name)"""
+    text = err if isinstance(err, str) else err.decode()
+    lines = text.splitlines(keepends=True)
+    engines = [ln.split("checksum engine ")[1].split(",")[0] for ln in lines if "checksum engine " in ln]
+    rest = "".join(ln for ln in lines if not ln.startswith("[trace]"))
+    return (rest if isinstance(err, str) else rest.encode()), engines
+
+
 @pytest.mark.parametrize("engine", ["hip", "auto"])
 @pytest.mark.parametrize("name", TOOL_CASES)
 def test_tool_gpu_engine_matches_reference(tmp_path, datafile_cases, name, engine, monkeypatch):
+    """every golden datafile through the GPU engine (auto: with the GPU
+    start-up forced and waited for) -- and the tool's trace proves that the
+    HIP engine did the checksum"""
     from test_tool_cpu import expected, run_tool
-    monkeypatch.setenv("ZDBCRC_AUTO_START_GPU", "1")  # auto: start the GPU even for a small scan
+    monkeypatch.setenv("ZDBCRC_AUTO_START_GPU", "1")  # auto: start the GPU even for a small scan, and wait for it
+    monkeypatch.setenv("ZDBCRC_TOOL_TRACE", "1")
     out, err, code = run_tool(name, tmp_path, engine)
+    err, engines = split_trace(err)
     eout, eerr = expected(name)
     assert out == eout
     assert err == eerr
     assert code == {c["name"]: c for c in datafile_cases}[name]["exit"]
+    assert engines == ([] if name in NO_PAYLOAD_CASES else ["hip"])
 
 
 @pytest.fixture(scope="module")
@@ -367,11 +411,14 @@ def test_tool_gpu_256MiB_matches_reference(big_datafile, engine):
     path, ref = big_datafile
     from test_tool_cpu import TOOL
     p = subprocess.run([str(TOOL), f"--engine={engine}", str(path)], capture_output=True,
-                       env=dict(os.environ, TZ="UTC"), timeout=120)
+                       env=dict(os.environ, TZ="UTC", ZDBCRC_TOOL_TRACE="1"), timeout=120)
     t = re.compile(rb"\[\s*\d+\.\d{6}\]")
+    err, engines = split_trace(p.stderr)
     assert p.returncode == ref.returncode == 3
     assert t.sub(b"[T]", p.stdout) == t.sub(b"[T]", ref.stdout)
-    assert p.stderr == ref.stderr
+    assert err == ref.stderr
+    # hip: the GPU did it; auto: one 256 MiB file is below the start-up policy's threshold
+    assert engines == (["hip"] if engine == "hip" else ["cpu"])
 
 
 @pytest.fixture(scope="module", params=["max8MiB", "zipf160MiB"])
@@ -416,11 +463,14 @@ def test_tool_gpu_large_values_match_reference(large_value_datafile, engine):
     path, ref = large_value_datafile
     from test_tool_cpu import TOOL
     p = subprocess.run([str(TOOL), f"--engine={engine}", str(path)], capture_output=True,
-                       env=dict(os.environ, TZ="UTC", ZDBCRC_AUTO_START_GPU="1"), timeout=120)
+                       env=dict(os.environ, TZ="UTC", ZDBCRC_AUTO_START_GPU="1", ZDBCRC_TOOL_TRACE="1"),
+                       timeout=120)
     t = re.compile(rb"\[\s*\d+\.\d{6}\]")
+    err, engines = split_trace(p.stderr)
     assert p.returncode == ref.returncode
     assert t.sub(b"[T]", p.stdout) == t.sub(b"[T]", ref.stdout)
-    assert p.stderr == ref.stderr
+    assert err == ref.stderr
+    assert engines == ["hip"]
 
 
 @pytest.mark.parametrize("jobs", [1, 3])

@@ -155,6 +155,16 @@ def test_device_walk_bound_and_capacity(dev):
     want, _ = serial(img)
     assert small.computed[:5].cpu().numpy().view(np.uint32).tolist() == [w[3] for w in want[:5]]
     assert dev._walk_device(None, None, None, 1, 1, 0, None, None, None, None, 0, None, None, None, None) == -2
+    # a size query (capacity 0): the walk's count comes back with ENOSPC
+    q, _ = store(dev, [img], capacity=0)
+    with pytest.raises(dev.ZdbCrcError, match=f"{len(want)} records > capacity 0"):
+        q.scan(2048)
+    # a store too large for the launch grids is refused up front (2^24 files of one chunk)
+    assert dev._walk_device(st.image.data_ptr(), st.file_off.data_ptr(), st.file_len.data_ptr(), 1 << 24,
+                            1024, 1024, st.entry_off.data_ptr(), st.payload_off.data_ptr(),
+                            st.payload_len.data_ptr(), st.expected.data_ptr(), st.capacity,
+                            st.file_records.data_ptr(), st.file_status.data_ptr(), st.rewalks.data_ptr(),
+                            None) == -2
 
 
 @pytest.mark.parametrize("name", ["mixed", "zipf_small", "corrupt_payload", "corrupt_crc", "multi_errors",
