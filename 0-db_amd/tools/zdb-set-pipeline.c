@@ -25,16 +25,37 @@
  * same request stream (timestamps aside): tests/test_set_pipeline.py runs
  * the reference zdbd (oracle/_ref/zdbd/zdb) beside it.
  *
- *   usage: zdb-set-pipeline [--engine=hip|cpu|auto] [--datasize=BYTES] [--batch=N]
- *                           [--stats] <datadir>   < requests   > replies
+ *   usage: zdb-set-pipeline [--engine=hip|cpu|auto] [--mode=user|seq] [--api]
+ *                           [--datasize=BYTES] [--batch=N] [--stats] <datadir>
+ *                           < requests   > replies
  *
  * --engine=auto checksums a batch on the GPU when its values total at least
  * AUTO_GPU_MIN_BYTES and with the scalar engine below that (one 256 KiB value
  * costs 35 us through the GPU and 21 us on one core), and
  * runs on the scalar engine alone when no GPU is usable.
  *
- * Only SET key value (3 arguments, user-key mode) is handled; any other
- * command ends the run with exit status 2.  The datafiles are
+ * Handlers (the daemon's table, commands_set.c:285-290):
+ *   --mode=user  redis_set_handler_userkey, commands_set.c:76-171 (default)
+ *   --mode=seq   redis_set_handler_sequential, commands_set.c:173-283: the
+ *                key is index_next_id (index.c:404-408) unless the request
+ *                names an existing id (8 bytes, index_get_handler_sequential,
+ *                index_get.c:16-59), "-Invalid key, only update authorized"
+ *                otherwise; an update appends the replaced entry, flagged
+ *                deleted, at the next id (index_update_entry_sequential,
+ *                index_set.c:321-356), so that id is skipped; the reply is
+ *                the 8-byte id.
+ * Arguments (command_set, commands_set.c:292-323): 4 arguments carry an
+ * admin timestamp (timestamp_from_set, :16-29; every client is admin when
+ * zdbd runs without --admin, redis.c:903); any count but 3 or 4 is
+ * "-Unexpected arguments" (commands.c:25-29).
+ * --api: the embedded API's SET instead (zdb_api_set, api.c:268-306, and its
+ * handlers api.c:108-256): no RESP reply but one line per request (BUFFER
+ * <hex> / UP_TO_DATE / FAILURE <message> / INSERT_DENIED), "unchanged" on
+ * crc equality alone (api.c:129-131, :204-211: no length or memcmp check),
+ * timestamps from the clock, no argument-count or key-length checks (3-argument
+ * SETs with keys of at most 255 bytes only).
+ *
+ * Any other command ends the run with exit status 2.  The datafiles are
  * <datadir>/d<id>, created from d0 on.
  */
 #define _GNU_SOURCE
@@ -160,6 +181,39 @@ static idx_entry_t *idx_find(const uint8_t *k, uint8_t n, int insert) {
     return &g_idx[j];
 }
 
+/* sequential mode: entry id -> (crc, length, file, offset), or a deleted
+ * placeholder (the replaced entry an update appends at the next id) */
+typedef struct {
+    uint32_t crc, length, fileid;
+    uint64_t offset;
+    int deleted;
+} seq_entry_t;
+
+static seq_entry_t *g_seq;
+static uint64_t g_seq_n, g_seq_cap; /* g_seq_n = index_next_id */
+
+static seq_entry_t *seq_push(void) {
+    if (g_seq_n == g_seq_cap) {
+        g_seq_cap = g_seq_cap ? 2 * g_seq_cap : 1024;
+        g_seq = realloc(g_seq, g_seq_cap * sizeof(*g_seq));
+        if (!g_seq)
+            die("out of memory");
+    }
+    memset(&g_seq[g_seq_n], 0, sizeof(*g_seq));
+    return &g_seq[g_seq_n++];
+}
+
+/* index_get in sequential mode: an 8-byte id below the next id whose entry is live */
+static seq_entry_t *seq_find(const uint8_t *k, uint32_t n) {
+    if (n != 8)
+        return NULL;
+    uint64_t id;
+    memcpy(&id, k, 8);
+    if (id >= g_seq_n || g_seq[id].deleted)
+        return NULL;
+    return &g_seq[id];
+}
+
 /* ---- datafiles ------------------------------------------------------------- */
 
 typedef struct {
@@ -243,6 +297,8 @@ static int store_read_payload(store_t *s, const idx_entry_t *e, uint8_t *dst) {
 typedef struct {
     uint64_t key_off, val_off; /* offsets in the receive buffer */
     uint32_t klen, vlen;
+    int argc;                  /* 2..5 (argv[0] = SET) */
+    int64_t timestamp;         /* argc == 4: atoll(argv[3]) */
 } set_req_t;
 
 static int parse_int(const uint8_t *p, const uint8_t *end, long *v, const uint8_t **next) {
@@ -259,7 +315,8 @@ static int parse_int(const uint8_t *p, const uint8_t *end, long *v, const uint8_
     return 1;
 }
 
-/* one complete "*3 $3 SET $k key $v value" at p: 1 parsed, 0 incomplete, -1 bad */
+/* one complete "*N $3 SET $k key $v value [$t timestamp]" at p, N = 2..5:
+ * 1 parsed, 0 incomplete, -1 bad or another command */
 static int parse_set(const uint8_t *base, const uint8_t *p, const uint8_t *end, set_req_t *r, const uint8_t **next) {
     if (p >= end)
         return 0;
@@ -269,11 +326,11 @@ static int parse_set(const uint8_t *base, const uint8_t *p, const uint8_t *end, 
     int rc = parse_int(p + 1, end, &argc, &p);
     if (rc <= 0)
         return rc;
-    if (argc != 3)
+    if (argc < 2 || argc > 5)
         return -1;
-    const uint8_t *arg[3];
-    long len[3];
-    for (int i = 0; i < 3; i++) {
+    const uint8_t *arg[5];
+    long len[5] = {0, 0, 0, 0, 0};
+    for (int i = 0; i < argc; i++) {
         if (p >= end)
             return 0;
         if (*p != '$')
@@ -291,12 +348,22 @@ static int parse_set(const uint8_t *base, const uint8_t *p, const uint8_t *end, 
             return -1;
         p += 2;
     }
-    if (len[0] != 3 || strncasecmp((const char *)arg[0], "SET", 3) != 0)
+    if (!((len[0] == 3 && strncasecmp((const char *)arg[0], "SET", 3) == 0) ||
+          (len[0] == 4 && strncasecmp((const char *)arg[0], "SETX", 4) == 0)))
         return -1;
+    r->argc = (int)argc;
     r->key_off = (uint64_t)(arg[1] - base);
     r->klen = (uint32_t)len[1];
-    r->val_off = (uint64_t)(arg[2] - base);
-    r->vlen = (uint32_t)len[2];
+    r->val_off = argc > 2 ? (uint64_t)(arg[2] - base) : r->key_off;
+    r->vlen = argc > 2 ? (uint32_t)len[2] : 0;
+    r->timestamp = 0;
+    if (argc == 4) { /* timestamp_from_set: atoll of the argument (commands_set.c:22-23) */
+        char t[64];
+        const size_t tl = (size_t)len[3] < sizeof(t) - 1 ? (size_t)len[3] : sizeof(t) - 1;
+        memcpy(t, arg[3], tl);
+        t[tl] = 0;
+        r->timestamp = atoll(t);
+    }
     *next = p;
     return 1;
 }
@@ -306,6 +373,8 @@ static int parse_set(const uint8_t *base, const uint8_t *p, const uint8_t *end, 
 typedef struct {
     int use_gpu;  /* GPU engine loaded                        */
     int auto_min; /* --engine=auto: small batches on the CPU  */
+    int seq;      /* --mode=seq: the sequential handler        */
+    int api;      /* --api: zdb_api_set semantics and replies  */
     size_t batch;
     int stats;
     double t_crc, t_apply, t_crc_warm;
@@ -316,6 +385,7 @@ static void reply(FILE *out, const char *s, size_t n) {
     if (fwrite(s, 1, n, out) != n)
         die("reply write failed");
 }
+#define REPLY_LIT(out, lit) reply((out), (lit), sizeof(lit) - 1)
 
 static void process(run_t *run, store_t *st, const uint8_t *buf, set_req_t *req, size_t n, uint32_t *crc,
                     uint64_t *voff, uint32_t *vlen, FILE *out, uint8_t *cmpbuf) {
@@ -348,50 +418,133 @@ static void process(run_t *run, store_t *st, const uint8_t *buf, set_req_t *req,
     for (size_t i = 0; i < n; i++) {
         const uint8_t *key = buf + req[i].key_off;
         const uint32_t klen = req[i].klen, L = req[i].vlen;
-        if (klen > MAX_KEY) { /* command_set, commands_set.c:316-319 */
-            reply(out, "-Key too large\r\n", 16);
-            continue;
+        if (!run->api) {
+            /* command_set's checks (commands_set.c:295-311, commands.c:25-29) */
+            if (req[i].argc != 3 && req[i].argc != 4) {
+                REPLY_LIT(out, "-Unexpected arguments\r\n");
+                continue;
+            }
+            if (klen > MAX_KEY) {
+                REPLY_LIT(out, "-Key too large\r\n");
+                continue;
+            }
         }
-        idx_entry_t *e = klen ? idx_find(key, (uint8_t)klen, 0) : NULL;
-        /* datafile rotation before the handler (commands_set.c:370-373) */
+        /* the existing entry: index_get (commands_set.c:338-342; api.c:279-283) */
+        idx_entry_t *e = NULL;
+        seq_entry_t *q = NULL;
+        if (klen) {
+            if (run->seq)
+                q = seq_find(key, klen);
+            else
+                e = idx_find(key, (uint8_t)klen, 0);
+        }
+        const int exists = e || q;
+        const uint32_t ex_crc = e ? e->crc : q ? q->crc : 0, ex_len = e ? e->length : q ? q->length : 0;
+        /* datafile rotation before the handler (commands_set.c:370-373, api.c:299-303) */
         if (st->size + L > st->datasize) {
             store_write_all(st);
             close(st->fd);
             store_open(st, st->fileid + 1); /* root->previous carries over (data.c:283-315) */
         }
-        if (klen == 0) { /* the handler's check, commands_set.c:86-89 */
-            reply(out, "-Invalid argument, key needed\r\n", 31);
+        /* the handler's own first check */
+        if (!run->seq && klen == 0) { /* commands_set.c:85-88, api.c:109-110 */
+            if (run->api)
+                REPLY_LIT(out, "FAILURE Invalid argument, key needed\n");
+            else
+                REPLY_LIT(out, "-Invalid argument, key needed\r\n");
             continue;
         }
-        /* unchanged payload: crc, then length and bytes (commands_set.c:52-74, :111-116) */
-        if (e && e->crc == crc[i] && e->length == L && store_read_payload(st, e, cmpbuf) &&
-            memcmp(cmpbuf, buf + voff[i], L) == 0) {
-            reply(out, "$-1\r\n", 5);
-            run->unchanged++;
+        if (run->seq && klen && !exists) { /* commands_set.c:182-185, api.c:178-179 */
+            if (run->api)
+                REPLY_LIT(out, "INSERT_DENIED\n");
+            else
+                REPLY_LIT(out, "-Invalid key, only update authorized\r\n");
             continue;
+        }
+        /* unchanged payload: the daemon checks crc, then length and bytes
+         * (commands_set.c:52-74, :111-116, :221-227); the API the crc alone
+         * (api.c:129-131, :204-207) */
+        if (exists && ex_crc == crc[i]) {
+            int same = run->api;
+            if (!same && ex_len == L) {
+                idx_entry_t tmp;
+                const idx_entry_t *src = e;
+                if (q) {
+                    tmp.klen = 8;
+                    tmp.length = q->length;
+                    tmp.fileid = q->fileid;
+                    tmp.offset = q->offset;
+                    src = &tmp;
+                }
+                same = store_read_payload(st, src, cmpbuf) && memcmp(cmpbuf, buf + voff[i], L) == 0;
+            }
+            if (same) {
+                if (run->api)
+                    REPLY_LIT(out, "UP_TO_DATE\n");
+                else
+                    REPLY_LIT(out, "$-1\r\n");
+                run->unchanged++;
+                continue;
+            }
+        }
+        /* the key written: the user's, or the sequential id (index_next_id,
+         * or the existing entry's id on an update) */
+        uint8_t idbuf[8];
+        const uint8_t *wkey = key;
+        uint32_t wklen = klen;
+        uint64_t id = g_seq_n;
+        if (run->seq) {
+            if (q)
+                id = (uint64_t)(q - g_seq);
+            memcpy(idbuf, &id, 8);
+            wkey = idbuf;
+            wklen = 8;
         }
         /* data_insert (data.c:594-633): header with this batch's crc, key, payload */
+        const uint32_t ts = (uint32_t)(req[i].argc == 4 ? req[i].timestamp : (int64_t)time(NULL));
         const uint64_t offset = st->size;
-        uint8_t *dst = store_reserve(st, ZDB_ENTRY_HEADER_SIZE + klen + L);
-        const size_t hl = zdb_datafile_encode_entry(dst, key, (uint8_t)klen, L, st->previous, crc[i], 0,
-                                                    (uint32_t)time(NULL));
+        uint8_t *dst = store_reserve(st, ZDB_ENTRY_HEADER_SIZE + wklen + L);
+        const size_t hl = zdb_datafile_encode_entry(dst, wkey, (uint8_t)wklen, L, st->previous, crc[i], 0, ts);
         memcpy(dst + hl, buf + voff[i], L);
         st->npend += hl + L;
         st->size += hl + L;
         st->previous = (uint32_t)offset;
-        /* index_set (commands_set.c:151) */
-        if (!e)
-            e = idx_find(key, (uint8_t)klen, 1);
-        e->crc = crc[i];
-        e->length = L;
-        e->fileid = st->fileid;
-        e->offset = offset;
-        /* reply: the key as a bulk string (commands_set.c:162-168) */
-        char head[32];
-        int hn = snprintf(head, sizeof(head), "$%u\r\n", klen);
-        reply(out, head, (size_t)hn);
-        reply(out, (const char *)key, klen);
-        reply(out, "\r\n", 2);
+        /* index_set (commands_set.c:151, :262) */
+        if (run->seq) {
+            if (q) { /* the replaced entry goes to the next id, flagged deleted */
+                seq_push()->deleted = 1;
+                q = &g_seq[id]; /* (seq_push may have moved the array) */
+            } else {
+                q = seq_push();
+            }
+            q->crc = crc[i];
+            q->length = L;
+            q->fileid = st->fileid;
+            q->offset = offset;
+        } else {
+            if (!e)
+                e = idx_find(key, (uint8_t)klen, 1);
+            e->crc = crc[i];
+            e->length = L;
+            e->fileid = st->fileid;
+            e->offset = offset;
+        }
+        /* reply: the key as a bulk string (commands_set.c:162-168, :274-280) */
+        if (run->api) {
+            static const char hx[] = "0123456789abcdef";
+            REPLY_LIT(out, "BUFFER ");
+            for (uint32_t b = 0; b < wklen; b++) {
+                const char c2[2] = {hx[wkey[b] >> 4], hx[wkey[b] & 15]};
+                reply(out, c2, 2);
+            }
+            REPLY_LIT(out, "\n");
+        } else {
+            char head[32];
+            int hn = snprintf(head, sizeof(head), "$%u\r\n", wklen);
+            reply(out, head, (size_t)hn);
+            reply(out, (const char *)wkey, wklen);
+            REPLY_LIT(out, "\r\n");
+        }
         run->bytes += L;
     }
     store_write_all(st); /* one append per batch */
@@ -420,6 +573,12 @@ int main(int argc, char **argv) {
             run.use_gpu = 1, run.auto_min = 0;
         else if (!strcmp(argv[argi], "--engine=auto"))
             run.use_gpu = 1, run.auto_min = 1;
+        else if (!strcmp(argv[argi], "--mode=user"))
+            run.seq = 0;
+        else if (!strcmp(argv[argi], "--mode=seq"))
+            run.seq = 1;
+        else if (!strcmp(argv[argi], "--api"))
+            run.api = 1;
         else if (!strncmp(argv[argi], "--datasize=", 11) && atoll(argv[argi] + 11) > 0)
             datasize = (uint64_t)atoll(argv[argi] + 11);
         else if (!strncmp(argv[argi], "--batch=", 8) && atol(argv[argi] + 8) > 0)
@@ -431,7 +590,9 @@ int main(int argc, char **argv) {
         argi++;
     }
     if (argc - argi != 1) {
-        fprintf(stderr, "Usage: %s [--engine=hip|cpu|auto] [--datasize=BYTES] [--batch=N] [--stats] <datadir>\n",
+        fprintf(stderr,
+                "Usage: %s [--engine=hip|cpu|auto] [--mode=user|seq] [--api] [--datasize=BYTES] [--batch=N] [--stats] "
+                "<datadir>\n",
                 argv[0]);
         return 1;
     }

@@ -707,6 +707,17 @@ def test_set_pipeline_gpu_engine_matches_reference_daemon(tmp_path, batch, datas
         assert without_clock(files[name]) == without_clock(ref_files[name]), name
 
 
+def test_set_pipeline_gpu_seq_mode_timestamps_and_api(tmp_path):
+    """a9 with the GPU engine: the sequential handler and timestamped /
+    malformed SETs against the reference zdbd started in sequential and user
+    mode, and zdb_api_set's crc-only UP_TO_DATE against the reference library
+    (tests/test_set_pipeline.py check_extra_modes)"""
+    from test_set_pipeline import API_REF, ZDBD, check_extra_modes
+    if not (ZDBD.exists() and API_REF.exists()):
+        pytest.skip("oracle/_ref not built")
+    check_extra_modes(tmp_path, "hip", batch=16)
+
+
 @pytest.mark.parametrize("engine", ["hip", "auto"])
 def test_set_pipeline_gpu_large_values(tmp_path, engine):
     """values up to the 8 MiB maximum payload (data.h:6) through the GPU

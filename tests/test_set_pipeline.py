@@ -27,11 +27,25 @@ import zdbcrc
 from conftest import ROOT
 
 ZDBD = Path(oracle.__file__).resolve().parent / "_ref" / "zdbd" / "zdb"
+API_REF = Path(oracle.__file__).resolve().parent / "_ref" / "api_set_ref"
 HARNESS = ROOT / "0-db_amd" / "bin" / "zdb-set-pipeline"
 
 
 def resp_set(key: bytes, value: bytes) -> bytes:
     return b"*3\r\n$3\r\nSET\r\n$%d\r\n%s\r\n$%d\r\n%s\r\n" % (len(key), key, len(value), value)
+
+
+def resp_cmd(*args: bytes) -> bytes:
+    return b"*%d\r\n" % len(args) + b"".join(b"$%d\r\n%s\r\n" % (len(a), a) for a in args)
+
+
+def seq_key(i: int) -> bytes:
+    return int(i).to_bytes(8, "little")
+
+
+# timestamps the requests carry (4-argument SET): far from the wall clock,
+# so the comparison can tell them from the clock-stamped entries
+TS_BASE = 4_000_000_000
 
 
 def build_stream(seed: int, n: int = 400):
@@ -79,6 +93,56 @@ def build_stream_large(seed: int, n: int = 24):
     return b"".join(out), n
 
 
+def build_stream_extra(seed: int, seq: bool, n: int = 160):
+    """SET variants beyond 3-argument user-key SETs: 4-argument SETs with an
+    admin timestamp (commands_set.c:295-300, timestamp_from_set :16-29), 2-
+    and 5-argument SETs ("-Unexpected arguments"), the SETX alias; with
+    seq=True the sequential handler (commands_set.c:173-283): new ids (empty
+    key), updates of existing ids (new and identical values), and keys it
+    refuses -- an id past the next one, a 3-byte key, and the id an update
+    leaves behind for the replaced entry"""
+    rng = np.random.default_rng(seed)
+    out, nreq, last = [], 0, {}
+    nnew = 0
+    for i in range(n):
+        size = int(rng.choice([0, 1, 3, 17, 64, 500, 4096, 20000, 98304]))
+        v = oracle.splitmix_bytes(size, seed * 1000 + i).tobytes()
+        r = rng.random()
+        if seq:
+            if nnew < 8 or r < 0.45:
+                k, nnew = b"", nnew + 1
+            elif r < 0.75:
+                k = seq_key(int(rng.integers(0, 8)))  # ids 0..7: the first new SETs, never placeholders
+                if k in last and rng.random() < 0.3:
+                    v = last[k]
+            else:
+                k = seq_key(int(rng.integers(8, 8 + nnew)))  # may be an id or a placeholder
+        else:
+            k = b"u-%d" % int(rng.integers(0, n // 3))
+            if k in last and r < 0.15:
+                v = last[k]
+        if rng.random() < 0.25:
+            out.append(resp_cmd(b"SET", k, v, b"%d" % (TS_BASE + i)))
+        else:
+            out.append(resp_cmd(b"SETX" if i % 9 == 4 else b"SET", k, v))
+        last[k] = v
+        nreq += 1
+        if i in (n // 4, n // 2):
+            out.append(resp_cmd(b"SET", b"only-a-key"))
+            out.append(resp_cmd(b"SET", b"k", b"v", b"1", b"extra"))
+            nreq += 2
+        if seq and i == n // 3:
+            out.append(resp_set(seq_key(10 ** 6), b"past the next id"))
+            out.append(resp_set(b"abc", b"not an id"))
+            nreq += 2
+        if i == n // 5:  # equal crc, other bytes (leading zeros are free): the daemon stores it
+            k = seq_key(3) if seq else b"u-0"
+            out.append(resp_set(k, b"crc twin"))
+            out.append(resp_set(k, b"\0\0crc twin"))
+            nreq += 2
+    return b"".join(out), nreq
+
+
 def read_replies(data: bytes, count: int):
     """split RESP replies ($-1, $n + bulk, -error); None if incomplete"""
     out, p = [], 0
@@ -99,10 +163,10 @@ def read_replies(data: bytes, count: int):
     return out
 
 
-def run_reference_zdbd(stream: bytes, nreq: int, tmp: Path, datasize: int):
+def run_reference_zdbd(stream: bytes, nreq: int, tmp: Path, datasize: int, mode: str = "user"):
     d, i, sock = tmp / "zdata", tmp / "zindex", tmp / "zdb.sock"
     proc = subprocess.Popen([str(ZDBD), "--data", str(d), "--index", str(i), "--socket", str(sock),
-                             "--mode", "user", "--datasize", str(datasize)],
+                             "--mode", mode, "--datasize", str(datasize)],
                             stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
     try:
         t_end = time.time() + 20
@@ -137,12 +201,13 @@ def run_reference_zdbd(stream: bytes, nreq: int, tmp: Path, datasize: int):
 
 
 def run_harness(stream: bytes, tmp: Path, datasize: int, engine: str = "cpu", batch: int = 64,
-                from_file: bool = False):
+                from_file: bool = False, extra: tuple = ()):
     """from_file: the stream is stdin as a regular file, so one read takes all
     of it and batches are bounded by --batch alone (a pipe hands over 64 KiB
-    at a time)"""
-    out = tmp / f"harness_{engine}_{batch}"
-    args = [str(HARNESS), f"--engine={engine}", f"--datasize={datasize}", f"--batch={batch}", "--stats", str(out)]
+    at a time); extra: more harness options (--mode=seq, --api)"""
+    out = tmp / f"harness_{engine}_{batch}{''.join(x.strip('-').replace('=', '') for x in extra)}"
+    args = [str(HARNESS), f"--engine={engine}", f"--datasize={datasize}", f"--batch={batch}", "--stats", *extra,
+            str(out)]
     if from_file:
         src = tmp / f"stream_{engine}_{batch}"
         src.write_bytes(stream)
@@ -157,13 +222,97 @@ def run_harness(stream: bytes, tmp: Path, datasize: int, engine: str = "cpu", ba
 
 def without_clock(img: bytes) -> bytes:
     """zero the wall-clock fields: data_header_t created/opened and every
-    entry's timestamp"""
+    entry's timestamp taken from the clock (the timestamps 4-argument SETs
+    carry, TS_BASE and up, stay and must match)"""
     b = bytearray(img)
     b[8:24] = bytes(16)
     recs, _ = zdbcrc.datafile_walk(img)
     for h in recs["header_offset"]:
-        b[int(h) + 14:int(h) + 18] = bytes(4)
+        if int.from_bytes(img[int(h) + 14:int(h) + 18], "little") < TS_BASE:
+            b[int(h) + 14:int(h) + 18] = bytes(4)
     return bytes(b)
+
+
+def run_reference_api(stream: bytes, tmp: Path, datasize: int, mode: str):
+    """the reference zdb_api_set over the same stream (oracle/_ref/api_set_ref)"""
+    root = tmp / f"api_{mode}"
+    replies = tmp / f"api_{mode}.replies"
+    p = subprocess.run([str(API_REF), str(root), mode, str(datasize), str(replies)], input=stream,
+                       capture_output=True, timeout=120)
+    assert p.returncode == 0, p.stderr.decode()[-2000:]
+    files = {q.name: q.read_bytes() for q in sorted((root / "data" / "default").glob("d*"))}
+    return replies.read_bytes(), files
+
+
+def check_extra_modes(tmp: Path, engine: str, batch: int = 16):
+    """sequential mode and the SET variants (build_stream_extra) against the
+    reference daemon, then the embedded API's SET in both modes against the
+    reference library: replies and datafiles byte-identical (clock fields
+    aside)"""
+    for mode in ("seq", "user"):
+        stream, nreq = build_stream_extra(29 if mode == "seq" else 31, seq=mode == "seq")
+        sub = tmp / f"daemon_{mode}"
+        sub.mkdir()
+        reps, ref_files = run_reference_zdbd(stream, nreq, sub, 600_000, mode)
+        out, files, _ = run_harness(stream, sub, 600_000, engine, batch, extra=(f"--mode={mode}",))
+        assert out == b"".join(reps), mode
+        assert sorted(files) == sorted(ref_files) and len(files) > 1, mode
+        for name in files:
+            assert without_clock(files[name]) == without_clock(ref_files[name]), (mode, name)
+        assert b"-Unexpected arguments\r\n" in out
+        if mode == "seq":
+            assert b"-Invalid key, only update authorized\r\n" in out and b"$8\r\n" in out and b"$-1\r\n" in out
+    for mode in ("user", "seq"):
+        stream, nreq = build_stream(41) if mode == "user" else build_stream_api_seq(43)
+        stream = b"".join(resp_set(k, v) for k, v in iter_sets(stream) if len(k) <= 255)
+        # equal crc, other bytes (crc(0^k || A) = crc(A)): the API keeps the old value (api.c:129-131)
+        k = seq_key(2) if mode == "seq" else b"twin"
+        stream += resp_set(k, b"crc twin") + resp_set(k, b"\0\0\0crc twin") + resp_set(k, b"other")
+        sub = tmp / f"api_{mode}"
+        sub.mkdir()
+        ref_out, ref_files = run_reference_api(stream, sub, 600_000, mode)
+        out, files, _ = run_harness(stream, sub, 600_000, engine, batch, extra=(f"--mode={mode}", "--api"))
+        assert out == ref_out, mode
+        assert sorted(files) == sorted(ref_files), mode
+        for name in files:
+            assert without_clock(files[name]) == without_clock(ref_files[name]), (mode, name)
+        assert b"UP_TO_DATE\n" in out
+
+
+def iter_sets(stream: bytes):
+    """(key, value) of every 3-argument SET of a stream"""
+    p = 0
+    while p < len(stream):
+        assert stream[p:p + 4] == b"*3\r\n"
+        p += 4
+        args = []
+        for _ in range(3):
+            e = stream.index(b"\r\n", p)
+            n = int(stream[p + 1:e])
+            args.append(stream[e + 2:e + 2 + n])
+            p = e + 2 + n + 2
+        yield args[1], args[2]
+
+
+def build_stream_api_seq(seed: int, n: int = 150):
+    """sequential-mode API SETs: new ids, updates with new values and with
+    values of equal crc (UP_TO_DATE), unknown ids (INSERT_DENIED)"""
+    rng = np.random.default_rng(seed)
+    out, last = [], {}
+    for i in range(n):
+        v = oracle.splitmix_bytes(int(rng.choice([0, 5, 64, 4096, 30000])), seed * 1000 + i).tobytes()
+        r = rng.random()
+        if i < 8 or r < 0.4:
+            k = b""
+        elif r < 0.9:
+            k = seq_key(int(rng.integers(0, 8)))
+            if k in last and rng.random() < 0.4:
+                v = last[k]
+        else:
+            k = seq_key(10 ** 6 + i)
+        last[k] = v
+        out.append(resp_set(k, v))
+    return b"".join(out), n
 
 
 needs_ref = pytest.mark.skipif(not ZDBD.exists(), reason="make -C oracle zdbd (needs /root/reference)")
@@ -207,6 +356,16 @@ def test_set_pipeline_datafiles_pass_reference_tool(tmp_path):
         os.symlink("d0", d / "zdb-data-0")
         p = subprocess.run([str(oracle.REF_INTEGRITY), str(d / "zdb-data-0")], capture_output=True, timeout=60)
         assert p.returncode == 0 and b"integrity check failed" not in p.stderr, name
+
+
+@needs_ref
+def test_set_pipeline_seq_mode_timestamps_and_api(tmp_path):
+    """a9 beyond the user-key handler: sequential mode, timestamped and
+    malformed SETs against the reference daemon, and zdb_api_set (crc-only
+    UP_TO_DATE) against the reference library -- scalar engine"""
+    if not API_REF.exists():
+        pytest.skip("make -C oracle ref (api_set_ref)")
+    check_extra_modes(tmp_path, "cpu")
 
 
 def test_set_pipeline_rejects_other_commands(tmp_path):
