@@ -146,9 +146,10 @@ __device__ __forceinline__ uint32_t look(const uint32_t *tab, int j, uint32_t a)
 // time (v_bitop3 xor3)
 // XM (A/B only): 0 = the windows above; 1 = timing diagnostic with one-op
 // extraction for every window (wrong checksums)
-template <int I, int XM = 0>
+// TOFF: dword offset of the slot tables in LDS (T; the packed kernel's TP)
+template <int I, int XM = 0, uint32_t TOFF = ZDBCRC_OFF_T>
 __device__ __forceinline__ uint32_t piece_contrib(const uint4 &v, const uint32_t *lds) {
-    const uint32_t *tab = lds + ZDBCRC_OFF_T + I * PCH * 32;
+    const uint32_t *tab = lds + TOFF + I * PCH * 32;
     const uint32_t w0 = v.x, w1 = v.y, w2 = v.z, w3 = v.w;
     if (XM == 3) { // timing diagnostic: the 16 A windows only (wrong checksums)
         uint32_t r = xor3(look(tab, 0, win(w0, 0)), look(tab, 1, win(w0, 1)), look(tab, 2, win(w0, 2)));
@@ -191,13 +192,18 @@ __device__ __forceinline__ uint32_t piece_contrib(const uint4 &v, const uint32_t
     return r;
 }
 
-// register advanced over one superstep (K KiB)
-__device__ __forceinline__ uint32_t advance_superstep(uint32_t a, const uint32_t *lds) {
+// register advanced over one superstep (tables at dword WOFF: W, K KiB; the
+// packed kernel's WP, 1 KiB)
+template <uint32_t WOFF>
+__device__ __forceinline__ uint32_t advance_superstep_at(uint32_t a, const uint32_t *lds) {
     uint32_t r = 0;
 #pragma unroll
     for (int c = 0; c < SCH; c++)
-        r ^= lds[ZDBCRC_OFF_W + c * 32 + ((a >> (5 * c)) & 31u)];
+        r ^= lds[WOFF + c * 32 + ((a >> (5 * c)) & 31u)];
     return r;
+}
+__device__ __forceinline__ uint32_t advance_superstep(uint32_t a, const uint32_t *lds) {
+    return advance_superstep_at<ZDBCRC_OFF_W>(a, lds);
 }
 
 // lane l's register shifted by 16*(63-l) bytes; [c][v][lane] layout: bank = lane
@@ -914,6 +920,479 @@ __global__ __launch_bounds__(WGT, WPE) void crc_batch_kernel_v3(
     }
 }
 
+// ---------------------------------------------------------------------------
+// packed small-record kernel: four records per wave, one per row of 16 lanes
+// ---------------------------------------------------------------------------
+//
+// The main kernel walks one record at a time with the whole wave, so a 4 KiB
+// value costs it one superstep plus everything a record boundary costs (lane
+// placement, reduction, metadata readlanes, segment bookkeeping: ~60 VALU and
+// ~140 SALU per record, the C2/C2u gap to C3; zipf_small in
+// profiles/r3/ab_split_small_large.jsonl: 2.96 us of wave time per record of
+// <= 4 KiB).  Here row g of a wave (lanes 16g .. 16g+15) walks a record of
+// its own: a slot is 256 B of it (16 lanes x 16 B), a superstep 1 KiB, and
+// the four rows of a packet share every instruction; a packet takes as many
+// supersteps as its longest record.  Placement, DPP reduction, fold and
+// store happen once per packet, not once per record.
+//
+// Grid of a record [A, E): the pieces end at Ep, the dword at or below E, so
+// every load is dword-aligned (byte-misaligned 16-byte loads stream ~19 %
+// slower, profiles/r2/misalign_probe.jsonl); the h = min(E & 3, L) bytes y
+// after Ep are folded in at the end, crc(X || y) = shift(crc(X) ^ y, h).
+// Piece 0 starts lo0 = 16 np - (L - h) bytes before A; those bytes are
+// masked.  Nothing is read past ceil4(E), and below A only inside piece 0 --
+// in A's 4 KiB page unless A lies in the first 16 bytes of a page: then piece
+// 0 is loaded from A's aligned block and moved up in registers (`d`, rare).
+//
+// Position q = 64 s + 16 i + l16 of a row's packet stream (superstep s, slot
+// i, lane l16) holds piece k = q - kb, kb = 64 S - np (k < 0: empty), loaded
+// from Ep - 16 (64 S - q).  Its contribution is shifted by 16 (64 S - 1 - q)
+// bytes: TP[i] carries 256 (3 - i), WP advances 1 KiB per superstep and LP
+// places lane l16 by 16 (15 - l16).  CPU model: tests/kernel_model.py
+// packed_batch.
+//
+// Work split: the planner's unit prefix (pieces + UO_PK per record); a wave
+// owns the records whose first unit lies in its slice (records are never
+// cut, so there are no atomics), then claims chunks of a tail pool as the
+// main kernel does.  Every step issues the same vector-memory instructions
+// (next packet's descriptors, 4 payload loads, the fold dword, one store --
+// to a dummy word when no packet ends) so that the compiler's vmcnt waits are
+// exact on every path: a wait merged over paths of different counts would
+// stall on loads issued a moment earlier.
+
+constexpr uint32_t UO_PK = 48; // planning charge per record (units = 16-byte pieces)
+#ifndef PK_SCHED_BARRIER
+#define PK_SCHED_BARRIER 1 // slots folded one after the other (keeps the kernel within 80 VGPRs)
+#endif
+constexpr uint32_t PK_F = 0;   // dword offsets inside the packed kernel's LDS image
+constexpr uint32_t PK_TP = ZDBCRC_OFF_TP - ZDBCRC_OFF_F;
+constexpr uint32_t PK_WP = ZDBCRC_OFF_WP - ZDBCRC_OFF_F;
+constexpr uint32_t PK_LP = ZDBCRC_OFF_LP - ZDBCRC_OFF_F;
+static_assert(ZDBCRC_OFF_F % 4 == 0 && ZDBCRC_PK_LDS_DW % 4 == 0, "packed LDS image must be 16-byte granular");
+
+// one row's record in the current packet (uniform within the row)
+struct PkGeo {
+    uint64_t pb; // Ep - 1024 S + 16 l16: this lane's load address in superstep 0, slot 0
+    int32_t kb;  // 64 S - np: positions before it are empty
+    uint32_t fl; // lo0 | h << 4 | d << 8 | (Ep & 3) << 16
+};
+// the packet (wave-uniform)
+struct PkPacket {
+    uint64_t r0;  // record of row 0 (row g: r0 + g)
+    uint32_t nr;  // rows holding a record (1..4)
+    uint32_t S;   // supersteps
+    int32_t kmin; // smallest kb of the rows: slots wholly before it are empty
+    int32_t kmax; // largest kb: supersteps wholly after it need no edge checks
+    bool anyh;    // some row folds bytes
+    bool anyd;    // some row loads piece 0 the rare way
+    uint32_t y[4]; // each row's fold dword (scalar loads)
+};
+
+// per-row scalars -> this lane's row's value
+__device__ __forceinline__ uint32_t row_pick(uint32_t lane, uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
+    const uint32_t g = lane >> 4;
+    return g == 0 ? a : g == 1 ? b : g == 2 ? c : d;
+}
+__device__ __forceinline__ uint64_t row_pick64(uint32_t lane, uint64_t a, uint64_t b, uint64_t c, uint64_t d) {
+    const uint32_t g = lane >> 4;
+    return g == 0 ? a : g == 1 ? b : g == 2 ? c : d;
+}
+
+// descriptors of a packet's four rows (records r .. r + 3, clamped to the
+// batch), through the scalar cache: they cost no vector registers and no
+// vector-memory instructions
+struct PkMeta {
+    uint64_t o[4];
+    uint32_t l[4];
+};
+__device__ __forceinline__ void pk_meta(PkMeta &m, const uint64_t *__restrict__ offsets,
+                                        const uint32_t *__restrict__ lengths, uint64_t r, uint64_t n) {
+#pragma unroll
+    for (int g = 0; g < 4; g++) {
+        const uint64_t i = r + g < n ? r + g : n - 1;
+        m.o[g] = offsets[i];
+        m.l[g] = lengths[i];
+    }
+}
+
+
+__device__ __forceinline__ uint32_t max4rows(uint32_t v) {
+    const uint32_t a = __builtin_amdgcn_readlane(v, 0), b = __builtin_amdgcn_readlane(v, 16);
+    const uint32_t c = __builtin_amdgcn_readlane(v, 32), d = __builtin_amdgcn_readlane(v, 48);
+    const uint32_t x = a > b ? a : b, y = c > d ? c : d;
+    return x > y ? x : y;
+}
+
+// geometry of the packet whose row g holds record rg = r0 + g (A, L: its
+// descriptor; rows at or past rb are empty), and each row's fold dword
+// (scalar loads).  A row without pieces (L - h = 0) gets its grid on the
+// table image (`dummy`), so that the loads of its empty positions -- which
+// read piece 0's address, F0 = pb + 16 (kb - l16) -- stay inside mapped memory
+// even for an empty record at the very end of the arena.
+__device__ __forceinline__ void pk_geometry(uint64_t A, uint32_t L, uint64_t r0, uint64_t rb, uint32_t lane,
+                                            const uint32_t *dummy, PkGeo &g, PkPacket &p) {
+    const uint64_t rg = r0 + (lane >> 4);
+    const bool valid = rg < rb;
+    if (!valid)
+        L = 0;
+    const uint64_t E = A + L;
+    const uint32_t e3 = (uint32_t)E & 3u;
+    const uint32_t h = e3 < L ? e3 : L;
+    const uint64_t Ep = E - h;
+    const uint32_t Lp = L - h;
+    const uint32_t np = (Lp + 15u) >> 4;
+    const uint32_t lo0 = 16u * np - Lp;
+    uint32_t S = max4rows((np + 63u) >> 6);
+    S = S ? S : 1u;
+    const int32_t kb = (int32_t)(64u * S) - (int32_t)np;
+    const uint32_t kbu = (uint32_t)kb; // kb in [0, 64 S]: compare as unsigned
+    p.r0 = r0;
+    p.nr = rb - r0 < 4 ? (uint32_t)(rb - r0) : 4u;
+    p.S = S;
+    p.kmax = (int32_t)max4rows(kbu);
+    p.kmin = (int32_t)(~max4rows(~kbu));
+    const uint64_t F0 = Ep - 16ull * np;
+    const uint64_t fa = A & ~15ull;
+    const uint32_t d = (np && F0 < fa && (fa & 4095ull) == 0) ? (uint32_t)(fa - F0) : 0u;
+    p.anyh = __ballot(h != 0) != 0;
+    p.anyd = __ballot(d != 0) != 0;
+    const uint64_t ya = h ? (Ep & ~3ull) : reinterpret_cast<uint64_t>(dummy);
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+        const uint64_t a = ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(ya >> 32), 16 * r) << 32) |
+                           (uint32_t)__builtin_amdgcn_readlane((uint32_t)ya, 16 * r);
+        p.y[r] = *reinterpret_cast<const uint32_t *>(a);
+    }
+    const uint64_t Eg = np ? Ep : reinterpret_cast<uint64_t>(dummy); // then F0 = the table image
+    g.pb = Eg - 1024ull * S + 16ull * (lane & 15u);
+    g.kb = kb;
+    g.fl = lo0 | (h << 4) | (d << 8) | (((uint32_t)Ep & 3u) << 16);
+}
+
+// piece 0 of a row: the rare shifted load (d: the block holding A, moved up
+// by d bytes), then the lo0 bytes before the record cleared
+__device__ __forceinline__ uint4 pk_shift_up(uint4 v, uint32_t d) {
+    const uint64_t lo = ((uint64_t)v.y << 32) | v.x, hi = ((uint64_t)v.w << 32) | v.z;
+    uint64_t nlo, nhi;
+    if (d >= 8) {
+        nhi = lo << (8u * (d - 8u));
+        nlo = 0;
+    } else {
+        nhi = (hi << (8u * d)) | (lo >> (64u - 8u * d));
+        nlo = lo << (8u * d);
+    }
+    return make_uint4((uint32_t)nlo, (uint32_t)(nlo >> 32), (uint32_t)nhi, (uint32_t)(nhi >> 32));
+}
+
+template <bool UNSAFE>
+__device__ __forceinline__ uint4 pk_first_piece(uint4 v, uint32_t fl) {
+    if (UNSAFE) {
+        const uint32_t d = (fl >> 8) & 15u;
+        if (d)
+            v = pk_shift_up(v, d);
+    }
+    return mask_piece(v, (int)(fl & 15u), 16);
+}
+
+template <bool NTL>
+__device__ __forceinline__ uint4 pk_ld(uint64_t a) {
+    global_u32x4 *p = reinterpret_cast<global_u32x4 *>(a);
+    const u32x4 v = NTL ? __builtin_nontemporal_load(p) : *p;
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
+
+// the 4 payload loads of superstep s; EDGE: lanes at positions before their
+// row's record re-read piece 0 (pk_superstep zeroes them), which comes from
+// A's aligned block when it would start in the page below.  No load is
+// conditional: a lane that skipped one would keep its register's previous
+// value alive.  (CPU model of every address: tests/kernel_model.py
+// packed_row_crc, test_packed_loads_stay_in_bounds.)
+template <bool EDGE, bool NTL>
+__device__ __forceinline__ void pk_load(uint64_t pb, int32_t kb, uint32_t fl, uint32_t s, uint32_t lane,
+                                        uint4 (&buf)[K]) {
+    const uint64_t base = pb + 1024ull * s;
+    // piece 0's load address: F0 = Ep - 16 np, moved up to A's aligned block
+    // when it would start in the page below (d); the table image for a row
+    // without pieces
+    const uint64_t F0 = pb + (int64_t)16 * ((int64_t)kb - (int64_t)(lane & 15u)) + ((fl >> 8) & 15u);
+#pragma unroll
+    for (int i = 0; i < K; i++) {
+        uint64_t a = base + 256u * i;
+        if (EDGE) {
+            const int32_t k = (int32_t)(64u * s + 16u * i + (lane & 15u)) - kb;
+            a = k <= 0 ? F0 : a; // k == 0: F0 is piece 0 itself (or its safe block)
+        }
+        buf[i] = pk_ld<NTL>(a);
+    }
+}
+
+// superstep s of the packet folded into the lane register
+template <bool EDGE, bool UNSAFE>
+__device__ __forceinline__ uint32_t pk_superstep(const PkGeo &g, const PkPacket &p, uint32_t acc, const uint4 (&cur)[K],
+                                                 uint32_t s, uint32_t lane, const uint32_t *lds) {
+    if (s)
+        acc = advance_superstep_at<PK_WP>(acc, lds);
+#define ZDBCRC_PK_SLOT(I)                                                                           \
+    if (!EDGE) {                                                                                    \
+        acc ^= piece_contrib<I, 0, PK_TP>(cur[I], lds);                                             \
+    } else if ((int32_t)(64u * s + 16u * (I) + 15u) >= p.kmin) { /* not empty in every row */     \
+        const int32_t k = (int32_t)(64u * s + 16u * (I) + (lane & 15u)) - g.kb;                     \
+        uint4 v = cur[I];                                                                           \
+        if (k < 0)                                                                                  \
+            v = make_uint4(0, 0, 0, 0);                                                             \
+        else if (k == 0)                                                                            \
+            v = pk_first_piece<UNSAFE>(v, g.fl);                                                    \
+        acc ^= piece_contrib<I, 0, PK_TP>(v, lds);                                                  \
+    }                                                                                               \
+    if (PK_SCHED_BARRIER)                                                                           \
+        __builtin_amdgcn_sched_barrier(0);
+    ZDBCRC_PK_SLOT(0)
+    ZDBCRC_PK_SLOT(1)
+    ZDBCRC_PK_SLOT(2)
+    ZDBCRC_PK_SLOT(3)
+#undef ZDBCRC_PK_SLOT
+    return acc;
+}
+
+// the packet's crcs: lane placement in the row, DPP reduction over the row,
+// fold of the h bytes after the grid (every lane of a row ends with its crc)
+__device__ __forceinline__ uint32_t pk_finish(const PkGeo &g, const PkPacket &p, uint32_t acc, uint32_t lane,
+                                              const uint32_t *lds) {
+    uint32_t x = 0;
+#pragma unroll
+    for (int c = 0; c < SCH; c++)
+        x ^= lds[PK_LP + (c * 32 + ((acc >> (5 * c)) & 31u)) * 32 + (lane & 31u)];
+    x ^= __builtin_amdgcn_update_dpp(0u, x, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
+    x ^= __builtin_amdgcn_update_dpp(0u, x, 0x4E, 0xF, 0xF, false);  // quad_perm [2,3,0,1]
+    x ^= __builtin_amdgcn_update_dpp(0u, x, 0x124, 0xF, 0xF, false); // row_ror:4
+    x ^= __builtin_amdgcn_update_dpp(0u, x, 0x128, 0xF, 0xF, false); // row_ror:8
+    if (p.anyh) { // F[0] is the identity: rows without fold bytes pass through
+        const uint32_t h = (g.fl >> 4) & 3u;
+        const uint32_t y = row_pick(lane, p.y[0], p.y[1], p.y[2], p.y[3]);
+        x ^= (y >> (8u * ((g.fl >> 16) & 3u))) & ((1u << (8u * h)) - 1u);
+        uint32_t r = 0;
+#pragma unroll
+        for (int c = 0; c < SCH; c++)
+            r ^= lds[PK_F + (h * SCH + c) * 32 + ((x >> (5 * c)) & 31u)];
+        x = r;
+    }
+    return x;
+}
+
+// first index r in [lo, hi) with f(r) >= key (hi if none); f nondecreasing;
+// one vector load per round of the 64-way search
+template <class F>
+__device__ __forceinline__ uint64_t first_ge(uint64_t lo, uint64_t hi, uint64_t key, uint32_t lane, F f) {
+    while (lo < hi) {
+        const uint64_t step = (hi - lo + 63) >> 6;
+        const uint64_t idx = lo + (uint64_t)lane * step;
+        const uint64_t lt = __ballot(idx < hi && f(idx) < key);
+        if (!lt)
+            return lo;
+        const uint32_t L = 63u - (uint32_t)__clzll(lt);
+        const uint64_t nhi = lo + (uint64_t)(L + 1) * step;
+        lo += (uint64_t)L * step + 1;
+        hi = nhi < hi ? nhi : hi;
+    }
+    return lo;
+}
+
+// first record whose first unit is >= key: the block offsets in LDS first
+// (boff[b] = unit_start of block b's first record), then the one block
+__device__ __forceinline__ uint64_t pk_first_record(const UnitPrefix &us, uint64_t n, uint32_t nb, uint64_t key,
+                                                    uint32_t lane) {
+    if (!us.boff)
+        return first_ge(0, n, key, lane, [&](uint64_t r) { return us.local[r]; });
+    const uint64_t b1 = first_ge(0, nb, key, lane, [&](uint64_t b) { return us.boff[b]; });
+    if (b1 < nb && us.boff[b1] == key)
+        return b1 << us.lg < n ? b1 << us.lg : n;
+    const uint64_t b = b1 - 1; // b1 >= 1: boff[0] = 0 <= key
+    const uint64_t lo = b << us.lg, hi = ((b + 1) << us.lg) < n ? ((b + 1) << us.lg) : n;
+    const uint64_t bo = us.boff[b];
+    return first_ge(lo, hi, key, lane, [&](uint64_t r) { return us.local[r] + bo; });
+}
+
+// WAITP: 1 = the next superstep's loads are issued once the previous ones
+// have landed (one superstep of loads in flight per wave); 0 = two
+
+template <int WGT, int WPE, int DYN = 4, int CPW = 4, uint32_t DYN_POOLS = 32, bool SP = true, int WAITP = 0,
+          bool NTL = true>
+__global__ __launch_bounds__(WGT, WPE) void crc_packed_kernel(
+    const uint8_t *__restrict__ arena, const uint64_t *__restrict__ offsets,
+    const uint32_t *__restrict__ lengths, const PlanArgs plan, uint64_t n,
+    uint32_t *__restrict__ out, const uint32_t *__restrict__ tables, uint32_t max_waves,
+    uint32_t *__restrict__ scratch, uint32_t epoch) {
+    constexpr uint32_t NW = WGT / 64;
+    if (plan.dn) {
+        const uint64_t dn = *plan.dn;
+        n = dn < n ? dn : n;
+    }
+    __shared__ __attribute__((aligned(16))) uint32_t lds[ZDBCRC_PK_LDS_DW];
+    __shared__ uint64_t boff[PLAN_MAX_BLOCKS + 1];
+    __shared__ uint64_t wsum[2 * NW + 1];
+
+    UnitPrefix unit_start{plan.local, nullptr, plan.lg};
+    if (plan.bsum) {
+        constexpr uint32_t PER = (PLAN_MAX_BLOCKS + WGT - 1) / WGT;
+        uint64_t v[PER], t = 0;
+#pragma unroll
+        for (uint32_t i = 0; i < PER; i++) {
+            const uint32_t b = threadIdx.x * PER + i;
+            v[i] = b < plan.nb ? plan.bsum[b] : 0;
+            t += v[i];
+        }
+        uint64_t total;
+        uint64_t e = block_excl_scan64<WGT>(t, wsum, &total);
+#pragma unroll
+        for (uint32_t i = 0; i < PER; i++) {
+            const uint32_t b = threadIdx.x * PER + i;
+            if (b <= plan.nb)
+                boff[b] = e;
+            e += v[i];
+        }
+        __syncthreads();
+        unit_start.boff = boff;
+    }
+
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t gw = __builtin_amdgcn_readfirstlane(blockIdx.x * NW + (threadIdx.x >> 6));
+    const uint64_t total = unit_start(n);
+    uint64_t nwaves = (total + MIN_UNITS_PER_WAVE - 1) / MIN_UNITS_PER_WAVE;
+    if (nwaves > max_waves)
+        nwaves = max_waves;
+    const bool dyn = DYN > 0 && gridDim.x >= DYN_POOLS && total >= DYN_MIN_UNITS_PER_WAVE * max_waves;
+    const uint64_t Ts = dyn ? total - total * DYN / 16 : total;
+    const uint32_t *const dummy = tables;
+
+    // the wave's first range: the records of its static slice (found before
+    // the table fill, so that the search's round trips overlap it)
+    uint64_t rb = 0, r0 = 0;
+    if (gw < nwaves) {
+        const uint64_t ub = Ts * gw / nwaves, ue = Ts * (gw + 1) / nwaves;
+        if (ub < ue) {
+            r0 = pk_first_record(unit_start, n, plan.nb, ub, lane);
+            rb = pk_first_record(unit_start, n, plan.nb, ue, lane);
+        }
+    }
+    {
+        const uint4 *src = reinterpret_cast<const uint4 *>(tables + ZDBCRC_OFF_F);
+        uint4 *dst = reinterpret_cast<uint4 *>(lds);
+        for (int i = threadIdx.x; i < ZDBCRC_PK_LDS_DW / 4; i += WGT)
+            dst[i] = src[i];
+    }
+    if (blockIdx.x == 0 && threadIdx.x < DYN_MAX_POOLS) // the next launch's counters (every variant)
+        scratch[SCRATCH_DYN_CTR + (((epoch + 1u) & 1u) * DYN_MAX_POOLS + threadIdx.x) * 32u] = 0u;
+    __syncthreads();
+
+    // tail pool, as crc_batch_kernel_v3 (pools drawn from every XCD)
+    const uint32_t pool = (blockIdx.x + blockIdx.x / DYN_POOLS) % DYN_POOLS;
+    const uint64_t Td = total - Ts;
+    const uint64_t P0 = Ts + Td * pool / DYN_POOLS;
+    const uint64_t PL = Ts + Td * (pool + 1) / DYN_POOLS - P0;
+    const uint64_t nch = (uint64_t)CPW * (nwaves / DYN_POOLS);
+    uint32_t *const ctr = scratch + SCRATCH_DYN_CTR + ((epoch & 1u) * DYN_MAX_POOLS + pool) * 32u;
+    if (SP && dyn)
+        __builtin_amdgcn_s_setprio(2);
+    uint32_t *const dwave = scratch + gw; // the store of a step without a finished packet
+
+    // Ranges (the static slice, then pool chunks), each walked packet by
+    // packet.  Within a range the loads of the next superstep -- this
+    // packet's next, or the next packet's first -- are issued before the
+    // current one is folded; every step issues the same vector-memory
+    // instructions in the same order (fold dword, next descriptors, payload,
+    // store), and the next packet's geometry is computed on every step and
+    // selected, so the loop carries each value in one place.
+    for (;;) {
+        if (r0 >= rb) { // next range from the pool
+            if (!(DYN && dyn))
+                return;
+            if (SP)
+                __builtin_amdgcn_s_setprio(0);
+            for (;;) {
+                uint32_t c = 0;
+                if (lane == 0)
+                    c = atomicAdd(ctr, 1u);
+                c = __builtin_amdgcn_readfirstlane(c);
+                if (c >= nch)
+                    return;
+                const uint64_t ub = P0 + PL * c / nch, ue = P0 + PL * (c + 1) / nch;
+                if (ue <= ub)
+                    continue;
+                r0 = pk_first_record(unit_start, n, plan.nb, ub, lane);
+                rb = pk_first_record(unit_start, n, plan.nb, ue, lane);
+                if (r0 < rb)
+                    break;
+            }
+        }
+        // descriptors of the range's first packet, then its geometry
+        PkMeta m;
+        pk_meta(m, offsets, lengths, r0, n);
+        const uint64_t ab = reinterpret_cast<uint64_t>(arena);
+        PkGeo gc;
+        PkPacket pc;
+        pk_geometry(ab + row_pick64(lane, m.o[0], m.o[1], m.o[2], m.o[3]), row_pick(lane, m.l[0], m.l[1], m.l[2], m.l[3]),
+                    r0, rb, lane, dummy, gc, pc);
+        uint4 cur[K], nxt[K];
+        // the loads of superstep s of packet (g, p); with its first superstep,
+        // the descriptors of the packet after it (scalar)
+        auto issue = [&](const PkGeo &g, PkPacket &p, uint32_t s, uint4(&buf)[K]) {
+            if (s == 0)
+                pk_meta(m, offsets, lengths, p.r0 + 4, n);
+            if ((int32_t)(64u * s) > p.kmax)
+                pk_load<false, NTL>(g.pb, g.kb, g.fl, s, lane, buf);
+            else
+                pk_load<true, NTL>(g.pb, g.kb, g.fl, s, lane, buf);
+        };
+        issue(gc, pc, 0, cur);
+        uint32_t css = 0, acc = 0;
+        for (;;) {
+            const bool newp = css + 1 == pc.S;
+            const bool last = newp && pc.r0 + 4 >= rb; // the range ends with this packet
+            PkGeo gn;
+            PkPacket pn;
+            const uint32_t nss = newp ? 0u : css + 1;
+            if (!last) {
+                if (WAITP)
+                    __builtin_amdgcn_s_waitcnt(0x0F70);
+                if (newp) {
+                    pk_geometry(ab + row_pick64(lane, m.o[0], m.o[1], m.o[2], m.o[3]),
+                                row_pick(lane, m.l[0], m.l[1], m.l[2], m.l[3]), pc.r0 + 4, rb, lane, dummy, gn, pn);
+                    issue(gn, pn, 0, nxt);
+                } else {
+                    issue(gc, pc, nss, nxt);
+                }
+            }
+            if ((int32_t)(64u * css) > pc.kmax)
+                acc = pk_superstep<false, false>(gc, pc, acc, cur, css, lane, lds);
+            else if (pc.anyd)
+                acc = pk_superstep<true, true>(gc, pc, acc, cur, css, lane, lds);
+            else
+                acc = pk_superstep<true, false>(gc, pc, acc, cur, css, lane, lds);
+            uint32_t *dst = dwave;
+            uint32_t x = 0;
+            if (newp) {
+                x = pk_finish(gc, pc, acc, lane, lds);
+                acc = 0;
+                if ((lane >> 4) < pc.nr)
+                    dst = out + pc.r0 + (lane >> 4);
+            }
+            if ((lane & 15u) == 0)
+                *dst = x;
+            if (last)
+                break;
+            if (newp) {
+                gc = gn;
+                pc = pn;
+            }
+            css = nss;
+#pragma unroll
+            for (int i = 0; i < K; i++)
+                cur[i] = nxt[i];
+        }
+        r0 = rb; // range done
+    }
+}
+
 typedef void (*crc_kernel_fn)(const uint8_t *, const uint64_t *, const uint32_t *, PlanArgs, uint64_t,
                               uint32_t *, const uint32_t *, uint32_t, uint32_t *, uint32_t);
 
@@ -979,6 +1458,13 @@ const KernelVariant kVariants[] = {
     {"v3_wg768_nt_dyn4c4p32_sp_uo512", crc_batch_kernel_v3<768, 6, false, 0, 512, false, true, false, 0, 4, 4, 32, true>, 768, WG_PER_CU, 512},
     {"v3_wg768_nt_dyn3c4p32_sp", crc_batch_kernel_v3<768, 6, false, 0, UNIT_OVH, false, true, false, 0, 3, 4, 32, true>, 768},
     {"v3_wg768_nt_dyn5c4p32_sp", crc_batch_kernel_v3<768, 6, false, 0, UNIT_OVH, false, true, false, 0, 5, 4, 32, true>, 768},
+    // round 3: the packed small-record kernel (four records per wave, one per row of 16 lanes)
+    {"pk_wg768_dyn4c4p32_sp", crc_packed_kernel<768, 6, 4, 4, 32, true, 0>, 768, WG_PER_CU, UO_PK},
+    {"pk_wg768_dyn4c4p32_sp_wait", crc_packed_kernel<768, 6, 4, 4, 32, true, 1>, 768, WG_PER_CU, UO_PK},
+    {"pk_wg640_dyn4c4p32_sp", crc_packed_kernel<640, 5, 4, 4, 32, true, 0>, 640, WG_PER_CU, UO_PK},
+    {"pk_wg640_dyn4c4p32_sp_wait", crc_packed_kernel<640, 5, 4, 4, 32, true, 1>, 640, WG_PER_CU, UO_PK},
+    {"pk_wg512_dyn4c4p32_sp", crc_packed_kernel<512, 4, 4, 4, 32, true, 0>, 512, WG_PER_CU, UO_PK},
+
 };
 constexpr int kNumVariants = (int)(sizeof(kVariants) / sizeof(kVariants[0]));
 std::atomic<int> g_variant{-1};

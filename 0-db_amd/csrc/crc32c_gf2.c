@@ -198,4 +198,28 @@ void zdbcrc_build_tables(uint32_t *img) {
             fill_linear(img + ZDBCRC_OFF_F + (h * ZDBCRC_SCH + c) * 32, 1, b);
         }
     }
+
+    /* packed kernel: rows of 16 lanes, 256 B per slot */
+    for (int i = 0; i < ZDBCRC_K; i++) {
+        const uint32_t m = xpow(8 * 256 * (uint64_t)(ZDBCRC_K - 1 - i), 0);
+        for (int c = 0; c < ZDBCRC_PCH; c++) {
+            for (int t = 0; t < 5; t++)
+                b[t] = multmodp(m, piece_window_crc(1u << t, c));
+            fill_linear(img + ZDBCRC_OFF_TP + (i * ZDBCRC_PCH + c) * 32, 1, b);
+        }
+    }
+    const uint32_t mwp = xpow(8 * 256 * (uint64_t)ZDBCRC_K, 0);
+    for (int c = 0; c < ZDBCRC_SCH; c++) {
+        for (int t = 0; t < 5; t++)
+            b[t] = multmodp(mwp, reg_slice(1u << t, c));
+        fill_linear(img + ZDBCRC_OFF_WP + c * 32, 1, b);
+    }
+    for (int l = 0; l < 32; l++) {
+        const uint32_t m = xpow(8 * 16 * (uint64_t)(15 - (l & 15)), 0);
+        for (int c = 0; c < ZDBCRC_SCH; c++) {
+            for (int t = 0; t < 5; t++)
+                b[t] = multmodp(m, reg_slice(1u << t, c));
+            fill_linear(img + ZDBCRC_OFF_LP + c * 32 * 32 + l, 32, b);
+        }
+    }
 }

@@ -52,7 +52,13 @@ uint32_t zdbcrc_update_bytes(uint32_t crc, const uint8_t *p, size_t n);
 #define ZDBCRC_OFF_Z    ZDBCRC_LDS_DW                                  /* [16][SCH][32]     */
 #define ZDBCRC_OFF_R    (ZDBCRC_OFF_Z + 16 * ZDBCRC_SCH * 32)          /* [RDIG][256][SCH][32] */
 #define ZDBCRC_OFF_F    (ZDBCRC_OFF_R + ZDBCRC_RDIG * 256 * ZDBCRC_SCH * 32) /* [4][SCH][32] */
-#define ZDBCRC_TABLE_DW (ZDBCRC_OFF_F + 4 * ZDBCRC_SCH * 32)
+/* packed small-record kernel (crc_packed_kernel): four records per wave, one
+ * per row of 16 lanes; its LDS image is the contiguous range [OFF_F, TABLE_DW) */
+#define ZDBCRC_OFF_TP   (ZDBCRC_OFF_F + 4 * ZDBCRC_SCH * 32)                /* [K][PCH][32]      */
+#define ZDBCRC_OFF_WP   (ZDBCRC_OFF_TP + ZDBCRC_K * ZDBCRC_PCH * 32)        /* [SCH][32]         */
+#define ZDBCRC_OFF_LP   (ZDBCRC_OFF_WP + ZDBCRC_SCH * 32)                   /* [SCH][32][32]     */
+#define ZDBCRC_TABLE_DW (ZDBCRC_OFF_LP + ZDBCRC_SCH * 32 * 32)
+#define ZDBCRC_PK_LDS_DW (ZDBCRC_TABLE_DW - ZDBCRC_OFF_F)
 
 /*
  * Piece windows.  A 16-byte piece (dwords w0..w3, little endian) is covered
@@ -85,6 +91,12 @@ int zdbcrc_window_bit(int j, int t);
  * F[h][c][v] : shift(v << 5c, h), h = 0..3     (a record-relative grid loaded
  *              from the dword below the record: its last h bytes y are folded
  *              in at the end as crc(X || y) = shift(crc(X) ^ y, h))
+ * Packed kernel (a row of 16 lanes walks one record, 256 B per slot, 1 KiB
+ * per superstep):
+ * TP[i][j][v]: as T, shifted by 256*(K-1-i) bytes
+ * WP[c][v]   : shift(v << 5c, 1024)           (row register across a superstep)
+ * LP[c][v][l]: shift(v << 5c, 16*(15-(l&15))), l = lane & 31 (lane l's
+ *              placement in its row; 32 columns so that bank = lane & 31)
  */
 void zdbcrc_build_tables(uint32_t *image /* ZDBCRC_TABLE_DW dwords */);
 

@@ -234,6 +234,37 @@ __device__ __forceinline__ bool plausible_successor(const uint8_t *f, uint64_t l
     return ld_le32(f + q + 5) == (uint32_t)p; // q's `previous` (data.h:59)
 }
 
+// relaxed confirmation (files whose `previous` fields do not chain, e.g. not
+// written by zdbd): the header at p and the RELAXED_HOPS headers its chain
+// leads to all pass the byte filter (datalength < 2^24, flags <= 3) and fit
+// in the file, or the chain ends exactly at the end of the file.  A random
+// position passes one hop with p ~ 2^-14, so three hops make a false start
+// practically impossible on non-adversarial data -- and a false start only
+// costs a serial re-walk: the stitch still checks every chunk start.
+constexpr int RELAXED_HOPS = 3;
+__device__ __forceinline__ bool forward_ok(const uint8_t *f, uint64_t len, uint64_t p) {
+    for (int hop = 0; hop <= RELAXED_HOPS; hop++) {
+        if (p == len)
+            return true;
+        if (p + ZDB_ENTRY_HEADER_SIZE > len)
+            return false;
+        const uintptr_t a = reinterpret_cast<uintptr_t>(f + p);
+        gu32 *q = reinterpret_cast<gu32 *>(a & ~uintptr_t(3));
+        const uint32_t sh = (uint32_t)(a & 3);
+        const uint32_t q0 = q[0], q1 = q[1], q2 = q[2], q3 = q[3], q4 = q[4];
+        const uint32_t w0 = __builtin_amdgcn_alignbyte(q1, q0, sh), w1 = __builtin_amdgcn_alignbyte(q2, q1, sh);
+        const uint32_t w3 = __builtin_amdgcn_alignbyte(q4, q3, sh);
+        const uint32_t idl = w0 & 0xFFu, L = (w0 >> 8) | (w1 << 24), flags = (w3 >> 8) & 0xFFu;
+        if ((L >> 24) != 0 || flags > 3u)
+            return false;
+        const uint64_t next = p + ZDB_ENTRY_HEADER_SIZE + idl + L;
+        if (next > len)
+            return false;
+        p = next;
+    }
+    return true;
+}
+
 struct FileTab {
     const uint8_t *image;
     const uint64_t *file_off;
@@ -271,7 +302,9 @@ __device__ __forceinline__ uint32_t from_next_lane(uint32_t own_next_row0, uint3
     return lane == 63 ? own_next_row0 : sh;
 }
 
-template <bool FWD, int SU, bool NOA1 = false>
+// RELAXED: candidates confirmed by forward_ok instead of the back-pointer
+// (and without the `previous` < p test)
+template <bool FWD, int SU, bool NOA1 = false, bool RELAXED = false>
 __device__ __forceinline__ uint64_t scan_block(const uint8_t *f, uint64_t len, uint64_t b, uint64_t lo, uint64_t hi,
                                                uint32_t lane) {
     uint4 a0[SU], a1[NOA1 ? 1 : SU], tl = make_uint4(~0u, ~0u, ~0u, ~0u);
@@ -332,7 +365,10 @@ __device__ __forceinline__ uint64_t scan_block(const uint8_t *f, uint64_t len, u
                     // the filter's false hits pass, so the header loads below
                     // stay rare
                     const uint32_t prev = r == 3 ? d[j + 2] : __builtin_amdgcn_alignbyte(d[j + 2], d[j + 1], r + 1);
-                    if (p >= lo && p < hi && (uint64_t)prev < p) {
+                    if (RELAXED) {
+                        if (p >= lo && p < hi && forward_ok(f, len, p))
+                            found = p;
+                    } else if (p >= lo && p < hi && (uint64_t)prev < p) {
                         const Hdr h = load_hdr(f, len, p);
                         if (plausible_successor(f, len, p, h.idl, h.L))
                             found = p; // positions rise within a lane: the last is the highest
@@ -446,6 +482,29 @@ __device__ __forceinline__ void search_chunk(const FileTab &t, uint64_t w, uint6
             back = false; // reached the datafile header
         if (done) {
             start = ans;
+            break;
+        }
+    }
+    if (start != NONE)
+        return;
+    // No header the back-pointer confirms starts in this chunk: either one
+    // entry covers it, or the file's `previous` fields do not chain (a file
+    // zdbd did not write) -- every chunk of such a file would otherwise be
+    // re-walked serially by the stitch.  Second pass, forward only, with the
+    // relaxed confirmation (forward_ok); zdbd's own files never get here
+    // unless a single entry spans the whole chunk.
+    for (uint64_t k = 0;; k++) {
+        const uint64_t b = c0 + (k * NWS + wid) * SB;
+        if (b < lim) {
+            const uint64_t found = scan_block<true, SU, NOA1, true>(f, len, b, c0, lim, lane);
+            if (found != NONE && lane == 0)
+                atomicMin(&bestf, (unsigned long long)found);
+        }
+        __syncthreads();
+        const uint64_t bf = bestf;
+        __syncthreads();
+        if (bf != NONE || c0 + (k + 1) * NWS * SB >= lim) {
+            start = bf;
             return;
         }
     }
