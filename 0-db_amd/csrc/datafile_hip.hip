@@ -87,6 +87,9 @@ constexpr bool WINDOW_CHAIN = true;
 // its own search is done, overlapping the other chunks' searches (C4 walk
 // 0.482 -> 0.421 ms in two A/B rounds, profiles/r2/walk_fused_ab.jsonl)
 constexpr bool FUSED_WALK = true;
+// chain window: 0 = the 1 KiB register window (chain_window), else the bytes
+// of the LDS-staged window (chain_wide)
+constexpr uint32_t CHAIN_WB = 0;
 
 // little-endian u32 at any byte address: two aligned dword loads + one
 // v_alignbyte (reads up to 7 bytes past p; images are readable 16 bytes past
@@ -667,6 +670,123 @@ __device__ __forceinline__ void chain_window(const FileTab &t, uint64_t w, uint6
     }
 }
 
+// the windowed chain with WB-byte windows staged through LDS (WB / 1024
+// 16-byte loads per lane; C4's median entry is ~300 bytes, so a wider window
+// decodes more of a chunk's headers without a new round trip: 1 / 2 / 4 /
+// 8 KiB windows take 68 / 55 / 45 / 37 window loads per 8 MiB chunk).  Lane l
+// loads window bytes [16 (l + 64 j), +16) for j < WB / 1024, each only when
+// its block starts at or before the file's end (the 16 readable bytes past
+// it), and writes them to the same offset of the wave's LDS window; a header
+// is then five uniform LDS dwords.  Same records, exits and terminal states
+// as chain_window.
+template <uint32_t WB> struct WideWindow {
+    static constexpr uint32_t NJ = WB / 1024;
+    uint4 v[NJ];
+    uintptr_t base;
+};
+
+template <uint32_t WB>
+__device__ __forceinline__ void load_wide(WideWindow<WB> &w, const uint8_t *f, uint64_t len, uint64_t pos,
+                                          uint32_t lane) {
+    w.base = reinterpret_cast<uintptr_t>(f + pos) & ~uintptr_t(15);
+    const uintptr_t end = reinterpret_cast<uintptr_t>(f + len);
+#pragma unroll
+    for (uint32_t j = 0; j < WideWindow<WB>::NJ; j++) {
+        const uintptr_t a = w.base + 16u * (lane + 64u * j);
+        w.v[j] = make_uint4(0, 0, 0, 0);
+        if (a <= end) {
+            typedef const __attribute__((address_space(1))) uint32_t gx4 __attribute__((ext_vector_type(4)));
+            const auto x = *reinterpret_cast<gx4 *>(a);
+            w.v[j] = make_uint4(x.x, x.y, x.z, x.w);
+        }
+    }
+}
+
+template <uint32_t WB>
+__device__ __forceinline__ void stage_wide(const WideWindow<WB> &w, uint32_t *lds, uint32_t lane) {
+#pragma unroll
+    for (uint32_t j = 0; j < WideWindow<WB>::NJ; j++)
+        *reinterpret_cast<uint4 *>(lds + 4u * (lane + 64u * j)) = w.v[j];
+    __builtin_amdgcn_wave_barrier();
+}
+
+__device__ __forceinline__ Hdr lds_hdr(const uint32_t *lds, uint32_t off) {
+    const uint32_t *q = lds + (off >> 2);
+    const uint32_t sh = off & 3u;
+    const uint32_t q0 = q[0], q1 = q[1], q2 = q[2], q3 = q[3], q4 = q[4];
+    const uint32_t w0 = __builtin_amdgcn_alignbyte(q1, q0, sh), w1 = __builtin_amdgcn_alignbyte(q2, q1, sh);
+    const uint32_t w2 = __builtin_amdgcn_alignbyte(q3, q2, sh), w3 = __builtin_amdgcn_alignbyte(q4, q3, sh);
+    return Hdr{w0 & 0xFFu, (w0 >> 8) | (w1 << 24), (w2 >> 8) | (w3 << 24)};
+}
+
+template <uint32_t WB>
+__device__ __forceinline__ void chain_wide(const FileTab &t, uint64_t w, uint64_t start, uint32_t lane,
+                                           uint64_t *__restrict__ s_exit, uint32_t *__restrict__ s_count,
+                                           int32_t *__restrict__ s_status, RecSlot *__restrict__ slots,
+                                           uint32_t kcap) {
+    __shared__ __attribute__((aligned(16))) uint32_t lds[WB / 4 + 4]; // + the 5th dword of a header at WB - 13
+    const uint32_t fi = (uint32_t)(w / t.cpf), c = (uint32_t)(w % t.cpf);
+    const uint64_t len = t.file_len[fi];
+    const uint8_t *f = t.image + t.file_off[fi];
+    const uint64_t cend = ((uint64_t)c + 1) << t.lg;
+    RecSlot *sl = slots + w * kcap;
+    uint32_t count = 0;
+    int32_t st = ST_CONTINUE;
+    uint64_t pos = start;
+    WideWindow<WB> win;
+    if (pos < cend && pos < len) {
+        load_wide<WB>(win, f, len, pos, lane);
+        stage_wide<WB>(win, lds, lane);
+    }
+    while (pos < cend) {
+        if (pos >= len) { // clean end of file (pos == len)
+            st = ZDB_WALK_OK;
+            break;
+        }
+        const Hdr h = lds_hdr(lds, (uint32_t)(reinterpret_cast<uintptr_t>(f + pos) - win.base));
+        const uint32_t hlen = ZDB_ENTRY_HEADER_SIZE + h.idl;
+        if (pos + hlen > len) {
+            st = ZDB_WALK_SHORT_HEADER;
+            break;
+        }
+        const uint32_t L = h.L;
+        uint64_t next = pos + hlen;
+        int32_t s = ST_CONTINUE;
+        if (L) {
+            if (next + L > len)
+                s = ZDB_WALK_SHORT_PAYLOAD;
+            else
+                next += L;
+        }
+        // the next window's loads are issued before the slot store (the
+        // memory counter completes in order) and staged after it
+        const bool reload = s == ST_CONTINUE && next < len && next < cend &&
+                            reinterpret_cast<uintptr_t>(f + next) - win.base + 13u > WB;
+        if (reload)
+            load_wide<WB>(win, f, len, next, lane);
+        __asm__ volatile("" ::: "memory");
+        if (count < kcap && lane == 0) {
+            const bool full = s == ST_CONTINUE && L > 0;
+            sl[count] = RecSlot{(uint32_t)pos, full ? L : 0u, full ? h.integ : 0u, hlen};
+        }
+        count++;
+        if (s == ZDB_WALK_SHORT_PAYLOAD) {
+            st = s;
+            break;
+        }
+        if (reload)
+            stage_wide<WB>(win, lds, lane);
+        pos = next;
+    }
+    if (st == ST_CONTINUE && pos >= len)
+        st = ZDB_WALK_OK;
+    if (lane == 0) {
+        s_exit[w] = pos;
+        s_count[w] = count;
+        s_status[w] = st;
+    }
+}
+
 __global__ __launch_bounds__(64) void walk_spec_win_kernel(FileTab t, const uint64_t *__restrict__ s_start,
                                                            uint64_t *__restrict__ s_exit,
                                                            uint32_t *__restrict__ s_count,
@@ -681,7 +801,7 @@ __global__ __launch_bounds__(64) void walk_spec_win_kernel(FileTab t, const uint
 // the chunk's chain as soon as its start is known, so the chains' round trips
 // overlap the searches of the other chunks (and the next workgroups' start)
 // instead of following all of them
-template <int NT, int SU, int MW>
+template <int NT, int SU, int MW, uint32_t WB = 0>
 __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MW))) void walk_search_chain_kernel(
     FileTab t, uint64_t *__restrict__ s_start, int32_t *__restrict__ s_status, uint64_t *__restrict__ s_exit,
     uint32_t *__restrict__ s_count, RecSlot *__restrict__ slots, uint32_t kcap) {
@@ -692,8 +812,12 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MW))) void w
         s_start[blockIdx.x] = start;
         s_status[blockIdx.x] = status;
     }
-    if (threadIdx.x < 64 && start != NONE)
-        chain_window(t, blockIdx.x, start, threadIdx.x, s_exit, s_count, s_status, slots, kcap);
+    if (threadIdx.x < 64 && start != NONE) {
+        if (WB)
+            chain_wide<WB ? WB : 1024>(t, blockIdx.x, start, threadIdx.x, s_exit, s_count, s_status, slots, kcap);
+        else
+            chain_window(t, blockIdx.x, start, threadIdx.x, s_exit, s_count, s_status, slots, kcap);
+    }
 }
 
 enum ChunkMode : uint32_t { MODE_NONE = 0, MODE_COPY = 1, MODE_WALK = 2 };
@@ -894,6 +1018,17 @@ int chain_mode() { // A/B: ZDBCRC_CHAIN_MODE (0: one lane per chunk, 1: one wave
     return v;
 }
 
+// A/B: ZDBCRC_CHAIN_WB or zdbcrc_debug_set_chain_wb (0: 1 KiB register
+// window, else LDS window bytes)
+int g_chain_wb = -1;
+uint32_t chain_wb() {
+    if (g_chain_wb < 0) {
+        const char *e = std::getenv("ZDBCRC_CHAIN_WB");
+        g_chain_wb = e ? std::atoi(e) : (int)CHAIN_WB;
+    }
+    return (uint32_t)g_chain_wb;
+}
+
 int search_variant() {
     static const int v = [] {
         const char *e = std::getenv("ZDBCRC_SEARCH_VARIANT");
@@ -989,10 +1124,26 @@ int zdb_datafile_walk_device(const uint8_t *d_image, const uint64_t *d_file_off,
 #else
     const bool fused = FUSED_WALK;
 #endif
-    if (fused)
-        hipLaunchKernelGGL((walk_search_chain_kernel<SEARCH_T, SEARCH_SU, SEARCH_MW>), dim3((uint32_t)nchunks),
-                           dim3(SEARCH_T), 0, st, t, s_start, s_status, s_exit, s_count, slots, kcap);
-    else {
+#ifdef ZDBCRC_DIAG
+    const uint32_t wb = chain_wb();
+#else
+    constexpr uint32_t wb = CHAIN_WB;
+#endif
+    if (fused) {
+#define ZDBCRC_FUSED(WBV)                                                                                              \
+    hipLaunchKernelGGL((walk_search_chain_kernel<SEARCH_T, SEARCH_SU, SEARCH_MW, WBV>), dim3((uint32_t)nchunks),       \
+                       dim3(SEARCH_T), 0, st, t, s_start, s_status, s_exit, s_count, slots, kcap)
+        switch (wb) {
+#ifdef ZDBCRC_DIAG
+        case 1024: ZDBCRC_FUSED(1024); break;
+        case 2048: ZDBCRC_FUSED(2048); break;
+        case 8192: ZDBCRC_FUSED(8192); break;
+#endif
+        case 4096: ZDBCRC_FUSED(4096); break;
+        default: ZDBCRC_FUSED(0); break;
+        }
+#undef ZDBCRC_FUSED
+    } else {
 #ifdef ZDBCRC_DIAG
     switch (search_variant()) { // A/B (scripts/walk_probe.py with the diagnostic library)
     case 9: hipLaunchKernelGGL((walk_search_kernel<256, 8, false>), dim3((uint32_t)nchunks), dim3(256), 0, st, t, s_start, s_status); break;
@@ -1046,6 +1197,14 @@ int zdb_datafile_walk_device(const uint8_t *d_image, const uint64_t *d_file_off,
 #ifdef ZDBCRC_DIAG
 // measurement/debug hook: the speculative and the true start of every chunk
 // of the last walk (device arrays copied to host; NONE = ~0)
+// A/B hook: the chain window of the fused walk (0, 1024, 2048, 4096, 8192)
+int zdbcrc_debug_set_chain_wb(int wb) {
+    if (wb != 0 && wb != 1024 && wb != 2048 && wb != 4096 && wb != 8192)
+        return -1;
+    g_chain_wb = wb;
+    return 0;
+}
+
 int zdbcrc_debug_walk_starts(uint64_t *s_start, uint64_t *true_start, uint64_t nchunks) {
     if (!g_last_walk.ws || nchunks != g_last_walk.nchunks)
         return -1;

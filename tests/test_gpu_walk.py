@@ -121,7 +121,58 @@ def test_device_walk_broken_previous_chain(dev):
     want, wst = serial(img)
     assert (int(status[0]), int(rec[1])) == (wst, len(want))
     assert walked(st, len(want)) == want
-    assert int(redo[-1]) > 0  # the serial fallback ran
+    # no back-pointer confirms a header: the relaxed second search found the
+    # chunk starts (the serial fallback: test_device_walk_unfiltered_headers)
+    assert int(redo[-1]) == 0
+
+
+def test_device_walk_scrambled_previous_256MiB(dev, tmp_path):
+    """f3's worst case: a 256 MiB reference-written datafile (65,000 x 4 KiB
+    values, oracle/_ref/gen_datafile_ref) whose `previous` fields are all
+    scrambled -- no back-pointer confirms any header, so every chunk used to
+    be re-walked serially (one dependent load per record).  The relaxed
+    second search (forward_ok: four headers in a row that parse and fit)
+    finds every chunk's start again: same records as the serial walk, no
+    re-walked chunk, and a walk time of the order of the host walk's.  The
+    timings land in gpurun_out/f3_worst_case.json."""
+    import json
+    import subprocess
+    import time
+    import oracle
+    import zdbcrc
+    if not oracle.REF_GEN.exists():
+        pytest.skip("oracle/_ref not built")
+    subprocess.run([str(oracle.REF_GEN), str(tmp_path), "fixed", "65000", "7", "4096"], check=True,
+                   capture_output=True)
+    img = np.fromfile(tmp_path / "data" / "default" / "d0", dtype=np.uint8).copy()
+    recs, _ = dev.datafile_walk(img)
+    rng = np.random.default_rng(3)
+    for h in recs["header_offset"]:
+        img[int(h) + 5:int(h) + 9] = rng.integers(0, 256, 4, dtype=np.uint8)
+    t0 = time.perf_counter()
+    zdbcrc.datafile_walk(img)  # the host walk (datafile.c), for scale
+    host_s = time.perf_counter() - t0
+    want, wst = serial(img)
+    st, _ = store(dev, [img])
+    st.walk()
+    torch.cuda.synchronize()
+    rec, status, redo = file_results(st)
+    assert (int(status[0]), int(rec[1])) == (wst, len(want)) and len(want) == 65000
+    assert walked(st, len(want)) == want
+    assert int(redo[-1]) == 0  # no chunk fell back to the serial re-walk
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ts = []
+    for _ in range(5):
+        ev0.record()
+        st.walk()
+        ev1.record()
+        torch.cuda.synchronize()
+        ts.append(ev0.elapsed_time(ev1))
+    out = ROOT / "gpurun_out"
+    out.mkdir(exist_ok=True)
+    (out / "f3_worst_case.json").write_text(json.dumps({
+        "file_bytes": int(len(img)), "records": len(want), "device_walk_ms": sorted(ts),
+        "host_walk_ms": round(host_s * 1e3, 2), "rewalked_chunks": int(redo[-1])}) + "\n")
 
 
 def test_device_walk_unfiltered_headers(dev):
