@@ -610,7 +610,7 @@ __device__ __forceinline__ bool in_window(const Window &w, const uint8_t *f, uin
 }
 
 // the windowed chain of chunk w from its speculative start (one wave)
-__device__ __forceinline__ void chain_window(const FileTab &t, uint64_t w, uint64_t start, uint32_t lane,
+__device__ __forceinline__ uint32_t chain_window(const FileTab &t, uint64_t w, uint64_t start, uint32_t lane,
                                              uint64_t *__restrict__ s_exit, uint32_t *__restrict__ s_count,
                                              int32_t *__restrict__ s_status, RecSlot *__restrict__ slots,
                                              uint32_t kcap) {
@@ -623,8 +623,11 @@ __device__ __forceinline__ void chain_window(const FileTab &t, uint64_t w, uint6
     int32_t st = ST_CONTINUE;
     uint64_t pos = start;
     Window win;
-    if (pos < cend && pos < len)
+    uint32_t loads = 0;
+    if (pos < cend && pos < len) {
         load_window(win, f, len, pos, lane);
+        loads++;
+    }
     while (pos < cend) {
         if (pos >= len) { // clean end of file (pos == len)
             st = ZDB_WALK_OK;
@@ -647,8 +650,10 @@ __device__ __forceinline__ void chain_window(const FileTab &t, uint64_t w, uint6
         }
         // the next header's window, when it is not this one (issued before the
         // slot store: the memory counter completes in order)
-        if (s == ST_CONTINUE && next < len && next < cend && !in_window(win, f, next))
+        if (s == ST_CONTINUE && next < len && next < cend && !in_window(win, f, next)) {
             load_window(win, f, len, next, lane);
+            loads++;
+        }
         __asm__ volatile("" ::: "memory");
         if (count < kcap && lane == 0) {
             const bool full = s == ST_CONTINUE && L > 0;
@@ -668,6 +673,7 @@ __device__ __forceinline__ void chain_window(const FileTab &t, uint64_t w, uint6
         s_count[w] = count;
         s_status[w] = st;
     }
+    return loads;
 }
 
 // the windowed chain with WB-byte windows staged through LDS (WB / 1024
@@ -720,7 +726,7 @@ __device__ __forceinline__ Hdr lds_hdr(const uint32_t *lds, uint32_t off) {
 }
 
 template <uint32_t WB>
-__device__ __forceinline__ void chain_wide(const FileTab &t, uint64_t w, uint64_t start, uint32_t lane,
+__device__ __forceinline__ uint32_t chain_wide(const FileTab &t, uint64_t w, uint64_t start, uint32_t lane,
                                            uint64_t *__restrict__ s_exit, uint32_t *__restrict__ s_count,
                                            int32_t *__restrict__ s_status, RecSlot *__restrict__ slots,
                                            uint32_t kcap) {
@@ -734,9 +740,11 @@ __device__ __forceinline__ void chain_wide(const FileTab &t, uint64_t w, uint64_
     int32_t st = ST_CONTINUE;
     uint64_t pos = start;
     WideWindow<WB> win;
+    uint32_t loads = 0;
     if (pos < cend && pos < len) {
         load_wide<WB>(win, f, len, pos, lane);
         stage_wide<WB>(win, lds, lane);
+        loads++;
     }
     while (pos < cend) {
         if (pos >= len) { // clean end of file (pos == len)
@@ -762,8 +770,10 @@ __device__ __forceinline__ void chain_wide(const FileTab &t, uint64_t w, uint64_
         // memory counter completes in order) and staged after it
         const bool reload = s == ST_CONTINUE && next < len && next < cend &&
                             reinterpret_cast<uintptr_t>(f + next) - win.base + 13u > WB;
-        if (reload)
+        if (reload) {
             load_wide<WB>(win, f, len, next, lane);
+            loads++;
+        }
         __asm__ volatile("" ::: "memory");
         if (count < kcap && lane == 0) {
             const bool full = s == ST_CONTINUE && L > 0;
@@ -785,6 +795,7 @@ __device__ __forceinline__ void chain_wide(const FileTab &t, uint64_t w, uint64_
         s_count[w] = count;
         s_status[w] = st;
     }
+    return loads;
 }
 
 __global__ __launch_bounds__(64) void walk_spec_win_kernel(FileTab t, const uint64_t *__restrict__ s_start,
@@ -801,10 +812,13 @@ __global__ __launch_bounds__(64) void walk_spec_win_kernel(FileTab t, const uint
 // the chunk's chain as soon as its start is known, so the chains' round trips
 // overlap the searches of the other chunks (and the next workgroups' start)
 // instead of following all of them
-template <int NT, int SU, int MW, uint32_t WB = 0>
+// STAMP (diagnostic library): per chunk, s_memrealtime (100 MHz) at the
+// start, after the search and after the chain, and the chain's window loads
+template <int NT, int SU, int MW, uint32_t WB = 0, bool STAMP = false>
 __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MW))) void walk_search_chain_kernel(
     FileTab t, uint64_t *__restrict__ s_start, int32_t *__restrict__ s_status, uint64_t *__restrict__ s_exit,
-    uint32_t *__restrict__ s_count, RecSlot *__restrict__ slots, uint32_t kcap) {
+    uint32_t *__restrict__ s_count, RecSlot *__restrict__ slots, uint32_t kcap, uint64_t *__restrict__ stamps) {
+    const uint64_t t0 = STAMP ? __builtin_amdgcn_s_memrealtime() : 0;
     uint64_t start;
     int32_t status;
     search_chunk<NT, SU, true>(t, blockIdx.x, start, status);
@@ -812,11 +826,24 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MW))) void w
         s_start[blockIdx.x] = start;
         s_status[blockIdx.x] = status;
     }
-    if (threadIdx.x < 64 && start != NONE) {
-        if (WB)
-            chain_wide<WB ? WB : 1024>(t, blockIdx.x, start, threadIdx.x, s_exit, s_count, s_status, slots, kcap);
-        else
-            chain_window(t, blockIdx.x, start, threadIdx.x, s_exit, s_count, s_status, slots, kcap);
+    if (threadIdx.x < 64) {
+        const uint64_t t1 = STAMP ? __builtin_amdgcn_s_memrealtime() : 0;
+        uint32_t loads = 0;
+        if (start != NONE) {
+            if (WB)
+                loads = chain_wide<WB ? WB : 1024>(t, blockIdx.x, start, threadIdx.x, s_exit, s_count, s_status,
+                                                   slots, kcap);
+            else
+                loads = chain_window(t, blockIdx.x, start, threadIdx.x, s_exit, s_count, s_status, slots, kcap);
+        }
+        if (STAMP && threadIdx.x == 0) {
+            const uint64_t t2 = __builtin_amdgcn_s_memrealtime();
+            uint64_t *sp = stamps + 4 * (uint64_t)blockIdx.x;
+            sp[0] = t0;
+            sp[1] = t1;
+            sp[2] = t2;
+            sp[3] = loads;
+        }
     }
 }
 
@@ -878,6 +905,7 @@ __device__ __forceinline__ void stitch_file(const FileTab &t, uint32_t fi, const
     rewalks[fi] = redo;
 }
 
+#ifdef ZDBCRC_DIAG // the round-2 stitch (one thread per file), for A/B
 __global__ __launch_bounds__(WALK_T) void walk_stitch_kernel(FileTab t, const uint64_t *__restrict__ s_start,
                                                              const uint64_t *__restrict__ s_exit,
                                                              const uint32_t *__restrict__ s_count,
@@ -909,6 +937,143 @@ __global__ __launch_bounds__(WALK_T) void walk_stitch_kernel(FileTab t, const ui
     }
 }
 
+#endif
+
+// B, one wave per file: every chunk's speculative result checked at once
+// (lane = chunk, 64 at a time).  The position that reaches chunk c is the
+// exit of the nearest chunk below it with a speculative start, or the
+// datafile header for chunk 0; the file is consistent when every live chunk
+// either starts exactly there or has no start and is reached at or past its
+// end (chunks after the first whose chain ended -- a terminal status -- are
+// dead, as in the serial stitch).  Consistent files (zdbd's, always, unless
+// one entry spans a chunk the search then mis-reads) get their chunk bases
+// from a wave prefix sum; any other file is stitched serially by lane 0
+// (stitch_file: the same outputs, by construction the reference order).
+__device__ __forceinline__ uint64_t shfl64(uint64_t v, uint32_t src) {
+    const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)v, (int)src, 64);
+    const uint32_t hi = (uint32_t)__shfl((int)(uint32_t)(v >> 32), (int)src, 64);
+    return ((uint64_t)hi << 32) | lo;
+}
+
+__device__ __forceinline__ uint64_t readlane64(uint64_t v, uint32_t l) {
+    return ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)(v >> 32), l) << 32) |
+           (uint32_t)__builtin_amdgcn_readlane((uint32_t)v, l);
+}
+
+__device__ __forceinline__ uint64_t wave_incl_scan64(uint64_t v, uint32_t lane) {
+#pragma unroll
+    for (uint32_t o = 1; o < 64; o <<= 1) {
+        const uint64_t u = shfl64(v, lane >= o ? lane - o : lane);
+        v += lane >= o ? u : 0;
+    }
+    return v;
+}
+
+__device__ __forceinline__ void stitch_file_wave(const FileTab &t, uint32_t fi, uint32_t lane,
+                                                 const uint64_t *__restrict__ s_start,
+                                                 const uint64_t *__restrict__ s_exit,
+                                                 const uint32_t *__restrict__ s_count,
+                                                 const int32_t *__restrict__ s_status, uint64_t *__restrict__ true_start,
+                                                 uint64_t *__restrict__ chunk_base, uint32_t *__restrict__ chunk_mode,
+                                                 uint32_t kcap, uint64_t *__restrict__ file_records,
+                                                 int32_t *__restrict__ file_status, uint32_t *__restrict__ rewalks) {
+    const uint64_t len = t.file_len[fi];
+    const uint64_t w0 = (uint64_t)fi * t.cpf;
+    bool ok = len <= ((uint64_t)t.cpf << t.lg) && s_status[w0] != ZDB_WALK_BAD_DESCRIPTOR;
+    uint64_t carry_pos = ZDB_DATA_HEADER_SIZE, total = 0;
+    bool carry_dead = false;
+    int32_t fst = ST_CONTINUE;
+    const uint64_t below_mask = (1ull << lane) - 1; // lanes under this one (lane 0: none)
+    for (uint32_t g = 0; ok && g < t.cpf; g += 64) {
+        const uint32_t c = g + lane;
+        const bool in = c < t.cpf;
+        const uint64_t w = w0 + c;
+        const uint64_t ss = in ? s_start[w] : NONE;
+        const bool act = ss != NONE;
+        const uint64_t ex = act ? s_exit[w] : 0;
+        const uint32_t cnt = act ? s_count[w] : 0u;
+        const int32_t cs = act ? s_status[w] : ST_CONTINUE;
+        const uint64_t am = __ballot(act);
+        const uint64_t tm = __ballot(act && cs != ST_CONTINUE);
+        const uint64_t below = am & below_mask;
+        const uint64_t pb_in = shfl64(ex, below ? 63u - (uint32_t)__clzll(below) : lane);
+        const uint64_t pb = below ? pb_in : carry_pos;
+        const bool dead = carry_dead || (tm & below_mask) != 0;
+        const uint64_t cend = ((uint64_t)c + 1) << t.lg;
+        const bool good = !in || dead || (act ? ss == pb : pb >= cend);
+        if (__ballot(!good)) {
+            ok = false;
+            break;
+        }
+        const bool walked = in && !dead && act;
+        const uint64_t v = walked ? cnt : 0;
+        const uint64_t incl = wave_incl_scan64(v, lane);
+        if (in) {
+            chunk_base[w] = total + incl - v;
+            true_start[w] = walked ? ss : NONE;
+            chunk_mode[w] = walked ? (cnt <= kcap ? MODE_COPY : MODE_WALK) : MODE_NONE;
+        }
+        total += readlane64(incl, 63);
+        const uint64_t twm = __ballot(walked && cs != ST_CONTINUE);
+        if (twm && fst == ST_CONTINUE)
+            fst = __builtin_amdgcn_readlane(cs, (uint32_t)__builtin_ctzll(twm));
+        if (am)
+            carry_pos = readlane64(ex, 63u - (uint32_t)__clzll(am));
+        carry_dead = carry_dead || tm != 0;
+    }
+    if (!ok) { // rewrites every output of the file (same wave: the stores above land first)
+        if (lane == 0)
+            stitch_file(t, fi, s_start, s_exit, s_count, s_status, true_start, chunk_base, chunk_mode, kcap,
+                        file_records, file_status, rewalks);
+        return;
+    }
+    if (lane == 0) {
+        file_records[fi] = total;
+        file_status[fi] = fst == ST_CONTINUE ? ZDB_WALK_OK : fst;
+        rewalks[fi] = 0;
+    }
+}
+
+// one wave per file; the last wave to finish (ticket counter, reset by it)
+// turns the per-file counts into the exclusive file prefix (entry nfiles =
+// total) and sums the re-walks, 64 files per step
+__global__ __launch_bounds__(64) void walk_stitch_wave_kernel(
+    FileTab t, const uint64_t *__restrict__ s_start, const uint64_t *__restrict__ s_exit,
+    const uint32_t *__restrict__ s_count, const int32_t *__restrict__ s_status, uint64_t *__restrict__ true_start,
+    uint64_t *__restrict__ chunk_base, uint32_t *__restrict__ chunk_mode, uint32_t kcap,
+    uint64_t *__restrict__ file_records, int32_t *__restrict__ file_status, uint32_t *__restrict__ rewalks,
+    uint32_t *__restrict__ done) {
+    const uint32_t lane = threadIdx.x;
+    stitch_file_wave(t, blockIdx.x, lane, s_start, s_exit, s_count, s_status, true_start, chunk_base, chunk_mode,
+                     kcap, file_records, file_status, rewalks);
+    __threadfence(); // this file's counts are visible device-wide before its ticket
+    uint32_t ticket = 0;
+    if (lane == 0)
+        ticket = atomicAdd(done, 1u);
+    ticket = (uint32_t)__shfl((int)ticket, 0, 64);
+    if (ticket != t.nfiles - 1)
+        return;
+    __threadfence(); // every other file's counts are visible here
+    uint64_t acc = 0;
+    uint32_t redo = 0;
+    for (uint32_t b = 0; b < t.nfiles; b += 64) {
+        const uint32_t i = b + lane;
+        const uint64_t n = i < t.nfiles ? file_records[i] : 0;
+        const uint32_t r = i < t.nfiles ? rewalks[i] : 0u;
+        const uint64_t incl = wave_incl_scan64(n, lane);
+        if (i < t.nfiles)
+            file_records[i] = acc + incl - n;
+        acc += readlane64(incl, 63);
+        redo += (uint32_t)readlane64(wave_incl_scan64(r, lane), 63);
+    }
+    if (lane == 0) {
+        file_records[t.nfiles] = acc;
+        rewalks[t.nfiles] = redo;
+        *done = 0; // for the next walk on this workspace (stream order)
+    }
+}
+
+#ifdef ZDBCRC_DIAG
 // B2: record counts -> global record base of every file, in place
 // (exclusive prefix; entry nfiles = total)
 __global__ void walk_prefix_kernel(uint32_t nfiles, uint64_t *__restrict__ file_records,
@@ -926,6 +1091,7 @@ __global__ void walk_prefix_kernel(uint32_t nfiles, uint64_t *__restrict__ file_
     file_records[nfiles] = acc;
     rewalks[nfiles] = redo;
 }
+#endif
 
 // C1: descriptors of the accepted chunks, copied from their slots (one
 // thread per slot)
@@ -1021,12 +1187,22 @@ int chain_mode() { // A/B: ZDBCRC_CHAIN_MODE (0: one lane per chunk, 1: one wave
 // A/B: ZDBCRC_CHAIN_WB or zdbcrc_debug_set_chain_wb (0: 1 KiB register
 // window, else LDS window bytes)
 int g_chain_wb = -1;
+uint64_t *g_stamps = nullptr;
+uint64_t g_stamps_n = 0, g_stamps_used = 0;
 uint32_t chain_wb() {
     if (g_chain_wb < 0) {
         const char *e = std::getenv("ZDBCRC_CHAIN_WB");
         g_chain_wb = e ? std::atoi(e) : (int)CHAIN_WB;
     }
     return (uint32_t)g_chain_wb;
+}
+
+bool serial_stitch() { // A/B: ZDBCRC_SERIAL_STITCH=1 -> one thread per file (the round-2 stitch)
+    static const bool v = [] {
+        const char *e = std::getenv("ZDBCRC_SERIAL_STITCH");
+        return e && std::atoi(e) == 1;
+    }();
+    return v;
 }
 
 int search_variant() {
@@ -1086,7 +1262,8 @@ int zdb_datafile_walk_device(const uint8_t *d_image, const uint64_t *d_file_off,
     // s_count, s_status, chunk_mode (4 B), kcap record slots (16 B each)
     const uint32_t kcap = nchunks <= 65536 ? 512u : 64u;
     auto al = [](size_t x) { return (x + 255) & ~size_t(255); };
-    const size_t need = 4 * al(nchunks * 8) + 3 * al(nchunks * 4) + al(nchunks * kcap * sizeof(RecSlot));
+    // (+ the stitch's ticket counter, zero between walks)
+    const size_t need = 4 * al(nchunks * 8) + 3 * al(nchunks * 4) + al(nchunks * kcap * sizeof(RecSlot)) + 256;
     WalkWs &ws = g_walk_ws[dev][stream];
     if (ws.bytes < need) {
         if (ws.ptr) {
@@ -1098,6 +1275,8 @@ int zdb_datafile_walk_device(const uint8_t *d_image, const uint64_t *d_file_off,
         if (hipMalloc(&ws.ptr, need) != hipSuccess)
             return ZDB_CRC32_ENOMEM;
         ws.bytes = need;
+        if (hipMemsetAsync(static_cast<uint8_t *>(ws.ptr) + need - 256, 0, 256, st) != hipSuccess)
+            return ZDB_CRC32_ELAUNCH;
     }
     uint8_t *b = static_cast<uint8_t *>(ws.ptr);
 #ifdef ZDBCRC_DIAG
@@ -1111,6 +1290,7 @@ int zdb_datafile_walk_device(const uint8_t *d_image, const uint64_t *d_file_off,
     int32_t *s_status = reinterpret_cast<int32_t *>(b + 4 * al(nchunks * 8) + al(nchunks * 4));
     uint32_t *chunk_mode = reinterpret_cast<uint32_t *>(b + 4 * al(nchunks * 8) + 2 * al(nchunks * 4));
     RecSlot *slots = reinterpret_cast<RecSlot *>(b + 4 * al(nchunks * 8) + 3 * al(nchunks * 4));
+    uint32_t *done = reinterpret_cast<uint32_t *>(b + ws.bytes - 256);
 
     const FileTab t{d_image, d_file_off, d_file_len, nfiles, (uint32_t)cpf64, lg};
 #ifdef ZDBCRC_DIAG
@@ -1132,7 +1312,21 @@ int zdb_datafile_walk_device(const uint8_t *d_image, const uint64_t *d_file_off,
     if (fused) {
 #define ZDBCRC_FUSED(WBV)                                                                                              \
     hipLaunchKernelGGL((walk_search_chain_kernel<SEARCH_T, SEARCH_SU, SEARCH_MW, WBV>), dim3((uint32_t)nchunks),       \
-                       dim3(SEARCH_T), 0, st, t, s_start, s_status, s_exit, s_count, slots, kcap)
+                       dim3(SEARCH_T), 0, st, t, s_start, s_status, s_exit, s_count, slots, kcap, nullptr)
+#ifdef ZDBCRC_DIAG
+#define ZDBCRC_FUSED_STAMP(WBV)                                                                                        \
+    hipLaunchKernelGGL((walk_search_chain_kernel<SEARCH_T, SEARCH_SU, SEARCH_MW, WBV, true>),                          \
+                       dim3((uint32_t)nchunks), dim3(SEARCH_T), 0, st, t, s_start, s_status, s_exit, s_count, slots,   \
+                       kcap, g_stamps)
+        if (g_stamps && nchunks <= g_stamps_n) {
+            g_stamps_used = nchunks;
+            if (wb == 2048)
+                ZDBCRC_FUSED_STAMP(2048);
+            else
+                ZDBCRC_FUSED_STAMP(0);
+        } else
+#undef ZDBCRC_FUSED_STAMP
+#endif
         switch (wb) {
 #ifdef ZDBCRC_DIAG
         case 1024: ZDBCRC_FUSED(1024); break;
@@ -1179,12 +1373,19 @@ int zdb_datafile_walk_device(const uint8_t *d_image, const uint64_t *d_file_off,
         hipLaunchKernelGGL(walk_spec_kernel, gchain, dim3(64), 0, st, t, s_start, s_exit, s_count, s_status, slots,
                            kcap, cpw);
     } // not fused
-    const bool one_block = nfiles <= WALK_T; // stitch and file prefix in one launch
-    hipLaunchKernelGGL(walk_stitch_kernel, dim3((nfiles + WALK_T - 1) / WALK_T), dim3(WALK_T), 0, st, t, s_start,
-                       s_exit, s_count, s_status, true_start, chunk_base, chunk_mode, kcap, d_file_records,
-                       d_file_status, d_rewalks, one_block);
-    if (!one_block)
-        hipLaunchKernelGGL(walk_prefix_kernel, dim3(1), dim3(64), 0, st, nfiles, d_file_records, d_rewalks);
+#ifdef ZDBCRC_DIAG
+    if (serial_stitch()) {
+        const bool one_block = nfiles <= WALK_T; // stitch and file prefix in one launch
+        hipLaunchKernelGGL(walk_stitch_kernel, dim3((nfiles + WALK_T - 1) / WALK_T), dim3(WALK_T), 0, st, t,
+                           s_start, s_exit, s_count, s_status, true_start, chunk_base, chunk_mode, kcap,
+                           d_file_records, d_file_status, d_rewalks, one_block);
+        if (!one_block)
+            hipLaunchKernelGGL(walk_prefix_kernel, dim3(1), dim3(64), 0, st, nfiles, d_file_records, d_rewalks);
+    } else
+#endif
+    hipLaunchKernelGGL(walk_stitch_wave_kernel, dim3(nfiles), dim3(64), 0, st, t, s_start, s_exit, s_count,
+                       s_status, true_start, chunk_base, chunk_mode, kcap, d_file_records, d_file_status, d_rewalks,
+                       done);
     if (capacity) {
         const uint64_t ncopy = (nchunks * kcap + WALK_T - 1) / WALK_T, nemit = (nchunks + WALK_T - 1) / WALK_T;
         hipLaunchKernelGGL(walk_out_kernel, dim3((uint32_t)(ncopy + nemit)), dim3(WALK_T), 0, st, t, true_start,
@@ -1197,6 +1398,17 @@ int zdb_datafile_walk_device(const uint8_t *d_image, const uint64_t *d_file_off,
 #ifdef ZDBCRC_DIAG
 // measurement/debug hook: the speculative and the true start of every chunk
 // of the last walk (device arrays copied to host; NONE = ~0)
+// measurement hook: stamp the next fused walks into a device buffer of n
+// chunks x 4 u64 (see walk_search_chain_kernel); returns the chunks stamped
+// by the last walk (0 to switch off: d_stamps == nullptr)
+uint64_t zdbcrc_debug_walk_stamps(uint64_t *d_stamps, uint64_t n) {
+    const uint64_t used = g_stamps_used;
+    g_stamps = d_stamps;
+    g_stamps_n = d_stamps ? n : 0;
+    g_stamps_used = 0;
+    return used;
+}
+
 // A/B hook: the chain window of the fused walk (0, 1024, 2048, 4096, 8192)
 int zdbcrc_debug_set_chain_wb(int wb) {
     if (wb != 0 && wb != 1024 && wb != 2048 && wb != 4096 && wb != 8192)
