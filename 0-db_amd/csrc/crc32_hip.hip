@@ -920,6 +920,7 @@ __global__ __launch_bounds__(WGT, WPE) void crc_batch_kernel_v3(
     }
 }
 
+#ifdef ZDBCRC_DIAG // measured, not shipped: profiles/r3/ab_packed_kernel.jsonl
 // ---------------------------------------------------------------------------
 // packed small-record kernel: four records per wave, one per row of 16 lanes
 // ---------------------------------------------------------------------------
@@ -1392,6 +1393,7 @@ __global__ __launch_bounds__(WGT, WPE) void crc_packed_kernel(
         r0 = rb; // range done
     }
 }
+#endif // ZDBCRC_DIAG (packed kernel)
 
 typedef void (*crc_kernel_fn)(const uint8_t *, const uint64_t *, const uint32_t *, PlanArgs, uint64_t,
                               uint32_t *, const uint32_t *, uint32_t, uint32_t *, uint32_t);
@@ -2021,7 +2023,8 @@ int wait_mailbox(HostStaging &h, uint32_t seq) {
 HostStaging g_host_staging[64];
 
 // pinned allocations made by zdb_crc32_host_alloc (base -> bytes, including
-// 64 readable bytes past what the caller asked for): a host-buffer batch
+// 64 readable bytes past what the caller asked for) and ranges pinned by
+// zdb_crc32_host_register (base -> bytes): a host-buffer batch
 // whose arena lies inside one is read by the kernel in place, over PCIe
 // (zero-copy), with no staging copy
 std::mutex g_pin_mu;
@@ -2040,6 +2043,17 @@ const uint8_t *pinned_device_view(const uint8_t *arena, size_t len) {
     if (hipHostGetDevicePointer(&dp, reinterpret_cast<void *>(it->first), 0) != hipSuccess || !dp)
         return nullptr;
     return static_cast<const uint8_t *>(dp) + (a - it->first);
+}
+
+// [p, p + n) inside one pinned range (allocated or registered)
+bool pinned_range(const uint8_t *p, size_t n) {
+    const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+    std::lock_guard<std::mutex> g(g_pin_mu);
+    auto it = g_pinned.upper_bound(a);
+    if (it == g_pinned.begin())
+        return false;
+    --it;
+    return a + n <= it->first + it->second;
 }
 
 size_t plan_bytes(size_t n) { return n * 8 + n * 4 + (n + 1) * 8 + n * 4 + 64; }
@@ -2460,6 +2474,27 @@ void zdb_crc32_host_free(void *p) {
     hipHostFree(p);
 }
 
+int zdb_crc32_host_register(void *p, size_t bytes) {
+    g_hip_touched = true;
+    if (!p || !bytes)
+        return ZDB_CRC32_EINVAL;
+    if (hipHostRegister(p, bytes, hipHostRegisterPortable | hipHostRegisterMapped) != hipSuccess)
+        return ZDB_CRC32_ENOMEM;
+    std::lock_guard<std::mutex> g(g_pin_mu);
+    g_pinned[reinterpret_cast<uintptr_t>(p)] = bytes;
+    return ZDB_CRC32_OK;
+}
+
+void zdb_crc32_host_unregister(void *p) {
+    if (!p)
+        return;
+    {
+        std::lock_guard<std::mutex> g(g_pin_mu);
+        g_pinned.erase(reinterpret_cast<uintptr_t>(p));
+    }
+    hipHostUnregister(p);
+}
+
 void zdb_crc32_set_timing(int enable) {
     std::lock_guard<std::mutex> g(g_mu);
     g_timing.store(enable != 0);
@@ -2614,6 +2649,15 @@ int zdb_crc32_stream_append(zdb_crc32_stream_t *s, const uint8_t *src, size_t n)
         return ZDB_CRC32_EINVAL;
     if (hipSetDevice(s->dev) != hipSuccess)
         return ZDB_CRC32_ELAUNCH;
+    if (n && pinned_range(src, n)) {
+        // pinned source (zdb_crc32_host_alloc / _register): one DMA straight
+        // from it, no staging copy and no wait -- the caller keeps the bytes
+        // until the next begin or checksum, which wait for the copy
+        if (hipMemcpyAsync(s->d_image + s->fill, src, n, hipMemcpyHostToDevice, s->st) != hipSuccess)
+            return ZDB_CRC32_ELAUNCH;
+        s->fill += n;
+        return ZDB_CRC32_OK;
+    }
     while (n) {
         const int i = s->next;
         // the slot is free again once its previous copy has left it

@@ -88,8 +88,16 @@ constexpr bool WINDOW_CHAIN = true;
 // 0.482 -> 0.421 ms in two A/B rounds, profiles/r2/walk_fused_ab.jsonl)
 constexpr bool FUSED_WALK = true;
 // chain window: 0 = the 1 KiB register window (chain_window), else the bytes
-// of the LDS-staged window (chain_wide)
-constexpr uint32_t CHAIN_WB = 0;
+// of the LDS-staged window (chain_wide).  C4 walk 0.432 (register) / 0.409
+// (1 KiB) / 0.407 (2 KiB) / 0.425 (4 KiB) / 0.446 ms (8 KiB),
+// profiles/r3/walk_chain_window_ab.jsonl
+constexpr uint32_t CHAIN_WB = 2048;
+// search filter in two passes (scan_block_ilp): no gain (C4 walk 0.423 ->
+// 0.434 ms, profiles/r3/walk_search_ilp_ab.jsonl)
+constexpr bool SEARCH_ILP = false;
+// skewed chunk edges (chunk_edge): C4 walk 0.414 -> 0.402 ms in three A/B
+// rounds (profiles/r3/walk_chunk_skew_ab.jsonl)
+constexpr bool CHUNK_SKEW = true;
 
 // little-endian u32 at any byte address: two aligned dword loads + one
 // v_alignbyte (reads up to 7 bytes past p; images are readable 16 bytes past
@@ -273,9 +281,25 @@ struct FileTab {
     const uint64_t *file_off;
     const uint64_t *file_len;
     uint32_t nfiles;
-    uint32_t cpf; // chunks per file (grid)
-    uint32_t lg;  // log2 chunk bytes
+    uint32_t cpf;  // chunks per file (grid)
+    uint32_t lg;   // log2 chunk bytes
+    uint32_t skew; // chunk edges moved down by up to 1/8 chunk (see chunk_edge)
 };
+
+// file-relative start of chunk c of file fi (c == cpf: the end of the last
+// chunk).  With t.skew, every inner edge moves down by a pseudo-random
+// multiple of 4 KiB below 1/8 chunk: the concurrent searches, which all start
+// at their chunk edge and step outward by the same block sizes, then spread
+// over the memory channels instead of hitting addresses equal modulo the
+// chunk size (edges stay increasing; any edges give the same walk -- the
+// stitch joins chunks whatever their bounds)
+__device__ __forceinline__ uint64_t chunk_edge(const FileTab &t, uint32_t fi, uint64_t c) {
+    const uint64_t e = c << t.lg;
+    if (!t.skew || c == 0 || c >= t.cpf || t.lg < 16)
+        return e;
+    const uint32_t h = (uint32_t)(((uint64_t)fi * t.cpf + c) * 0x9E3779B1u) >> 8;
+    return e - (uint64_t)(h % (1u << (t.lg - 15))) * 4096u;
+}
 
 // candidate positions among the 16 starting at a 16-byte block whose 32
 // bytes are d[0..7]: byte p+4 (top byte of datalength) is 0 and byte p+13
@@ -400,6 +424,109 @@ __device__ __forceinline__ uint64_t scan_block(const uint8_t *f, uint64_t len, u
     return x;
 }
 
+// one 1 KiB row of a scan block: this lane's 16 bytes, the next lane's 16
+// (lane 63: lane 0 of the next row, `next`, uniform after readlane) and the
+// filter of its 16 positions
+__device__ __forceinline__ void filter_row(const uint4 &cur, const uint4 &next, uint32_t lane, uint32_t (&d)[8],
+                                           uint32_t (&z)[4]) {
+    d[0] = cur.x;
+    d[1] = cur.y;
+    d[2] = cur.z;
+    d[3] = cur.w;
+    d[4] = from_next_lane(__builtin_amdgcn_readlane(next.x, 0), cur.x, lane);
+    d[5] = from_next_lane(__builtin_amdgcn_readlane(next.y, 0), cur.y, lane);
+    d[6] = from_next_lane(__builtin_amdgcn_readlane(next.z, 0), cur.z, lane);
+    d[7] = from_next_lane(__builtin_amdgcn_readlane(next.w, 0), cur.w, lane);
+    candidates(d, z);
+}
+
+// scan_block (NOA1 shape) in two passes: the byte filter over all SU rows
+// first, with no branch between them (the rows' dependency chains -- DPP
+// neighbour, readlane, filter -- interleave instead of ending each in a
+// ballot and a branch), then, only when some lane of the block has a
+// candidate, the confirmation row by row in address order as scan_block does.
+// Same result as scan_block<FWD, SU, true, RELAXED>.
+template <bool FWD, int SU, bool RELAXED = false, bool ILP_PAIR = true>
+__device__ __forceinline__ uint64_t scan_block_ilp(const uint8_t *f, uint64_t len, uint64_t b, uint64_t lo,
+                                                   uint64_t hi, uint32_t lane) {
+    uint4 a0[SU], tl = make_uint4(~0u, ~0u, ~0u, ~0u);
+#pragma unroll
+    for (int u = 0; u < SU; u++) {
+        const uint64_t p0 = b + 1024u * u + 16u * lane;
+        a0[u] = p0 + 32 > lo && p0 < hi + 16 ? *reinterpret_cast<const uint4 *>(f + p0)
+                                              : make_uint4(~0u, ~0u, ~0u, ~0u);
+    }
+    if (b + 1024u * SU < hi + 16) { // see scan_block: must stay a vector load
+        uint64_t ta = reinterpret_cast<uint64_t>(f + b + 1024u * SU);
+        __asm__ volatile("" : "+v"(ta));
+        tl = *reinterpret_cast<const uint4 *>(ta);
+    }
+    uint32_t any = 0;
+#pragma unroll
+    for (int u = 0; u < SU; u++) {
+        uint32_t d[8], z[4];
+        filter_row(a0[u], u + 1 < SU ? a0[u + 1 < SU ? u + 1 : u] : tl, lane, d, z);
+        any |= ((z[0] | z[1] | z[2] | z[3]) != 0u ? 1u : 0u) << u;
+        if (ILP_PAIR && (u & 1)) // at most two rows in flight (80 VGPRs)
+            __builtin_amdgcn_sched_barrier(0);
+    }
+    uint64_t found = FWD ? NONE : 0;
+    if (__ballot(any != 0u)) {
+#pragma unroll
+        for (int u = 0; u < SU; u++) {
+            if (!__ballot((any >> u) & 1u))
+                continue;
+            // the row's 32 bytes per lane again (L2-hot; keeping a0 live
+            // through this rare pass costs the hot pass its registers), with
+            // the first pass's bounds: ~0 where nothing was loaded
+            const uint64_t p0 = b + 1024u * u + 16u * lane;
+            uint4 x0 = make_uint4(~0u, ~0u, ~0u, ~0u), x1 = x0;
+            if (p0 + 32 > lo && p0 < hi + 16)
+                x0 = *reinterpret_cast<const uint4 *>(f + p0);
+            if (p0 + 48 > lo && p0 < hi)
+                x1 = *reinterpret_cast<const uint4 *>(f + p0 + 16);
+            uint32_t d[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w}, z[4];
+            candidates(d, z);
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                uint32_t m = z[j];
+                while (m && (!FWD || found == NONE)) {
+                    const uint32_t r = (uint32_t)__builtin_ctz(m) >> 3;
+                    m &= ~(0xFFu << (8 * r));
+                    const uint64_t p = p0 + 4u * j + r;
+                    const uint32_t prev =
+                        r == 3 ? d[j + 2] : __builtin_amdgcn_alignbyte(d[j + 2], d[j + 1], r + 1);
+                    if (RELAXED) {
+                        if (p >= lo && p < hi && forward_ok(f, len, p))
+                            found = p;
+                    } else if (p >= lo && p < hi && (uint64_t)prev < p) {
+                        const Hdr h = load_hdr(f, len, p);
+                        if (plausible_successor(f, len, p, h.idl, h.L))
+                            found = p;
+                    }
+                }
+            }
+            if (FWD) {
+                const uint64_t hit = __ballot(found != NONE);
+                if (hit) {
+                    const uint32_t l = (uint32_t)__builtin_ctzll(hit);
+                    return ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)(found >> 32), l) << 32) |
+                           (uint32_t)__builtin_amdgcn_readlane((uint32_t)found, l);
+                }
+            }
+        }
+    }
+    if (FWD)
+        return NONE;
+    uint32_t x = (uint32_t)found;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const uint32_t y = (uint32_t)__shfl_xor((int)x, o, 64);
+        x = y > x ? y : x;
+    }
+    return x;
+}
+
 // A1: speculative start of every chunk: the first entry header at or past the
 // chunk start c0 (one workgroup of NWS waves per chunk).  Half of the waves
 // search forward from c0 in interleaved SU-KiB blocks; the other half search
@@ -410,7 +537,7 @@ __device__ __forceinline__ uint64_t scan_block(const uint8_t *f, uint64_t len, u
 // the worst case.
 // the search of chunk w (one workgroup of NT threads); every thread returns
 // the chunk's speculative start and status
-template <int NT, int SU, bool NOA1>
+template <int NT, int SU, bool NOA1, bool ILP = false>
 __device__ __forceinline__ void search_chunk(const FileTab &t, uint64_t w, uint64_t &start, int32_t &status) {
     constexpr uint32_t NWS = NT / 64, NF = NWS / 2, NB = NWS - NF;
     constexpr uint64_t SB = 1024u * SU; // bytes per wave block
@@ -420,7 +547,7 @@ __device__ __forceinline__ void search_chunk(const FileTab &t, uint64_t w, uint6
     const uint32_t fi = (uint32_t)(w / t.cpf), c = (uint32_t)(w % t.cpf);
     const uint64_t len = t.file_len[fi];
     const uint8_t *f = t.image + t.file_off[fi];
-    const uint64_t C = 1ull << t.lg, c0 = (uint64_t)c * C;
+    const uint64_t c0 = chunk_edge(t, fi, c), c1 = chunk_edge(t, fi, (uint64_t)c + 1);
     status = ST_CONTINUE;
     if (c == 0) {
         // data_descriptor_load / _validate (data.c:177-209): 28-byte
@@ -434,8 +561,8 @@ __device__ __forceinline__ void search_chunk(const FileTab &t, uint64_t w, uint6
     start = NONE;
     if (c0 >= len || len < ZDB_ENTRY_HEADER_SIZE)
         return;
-    // positions p in [c0, c0 + C) with a whole 18-byte header in the file
-    const uint64_t lim = (c0 + C < len - (ZDB_ENTRY_HEADER_SIZE - 1)) ? c0 + C : len - (ZDB_ENTRY_HEADER_SIZE - 1);
+    // positions p in [c0, c1) with a whole 18-byte header in the file
+    const uint64_t lim = (c1 < len - (ZDB_ENTRY_HEADER_SIZE - 1)) ? c1 : len - (ZDB_ENTRY_HEADER_SIZE - 1);
     constexpr uint64_t LO = ZDB_DATA_HEADER_SIZE; // entries start at or after the datafile header
     if (threadIdx.x == 0) {
         bestf = NONE;
@@ -447,7 +574,8 @@ __device__ __forceinline__ void search_chunk(const FileTab &t, uint64_t w, uint6
         if (wid < NF) {
             const uint64_t b = c0 + (k * NF + wid) * SB;
             if (b < lim) {
-                const uint64_t found = scan_block<true, SU, NOA1>(f, len, b, c0, lim, lane);
+                const uint64_t found = ILP ? scan_block_ilp<true, SU>(f, len, b, c0, lim, lane)
+                                           : scan_block<true, SU, NOA1>(f, len, b, c0, lim, lane);
                 if (found != NONE && lane == 0)
                     atomicMin(&bestf, (unsigned long long)found);
             }
@@ -455,7 +583,8 @@ __device__ __forceinline__ void search_chunk(const FileTab &t, uint64_t w, uint6
             const uint64_t dist = (k * NB + (wid - NF) + 1) * SB; // block [c0 - dist, c0 - dist + SB)
             if (dist < c0 + SB && c0 + SB - dist > LO) {
                 const uint64_t b = c0 > dist ? c0 - dist : 0;
-                const uint64_t found = scan_block<false, SU, NOA1>(f, len, b, LO, c0, lane);
+                const uint64_t found = ILP ? scan_block_ilp<false, SU>(f, len, b, LO, c0, lane)
+                                           : scan_block<false, SU, NOA1>(f, len, b, LO, c0, lane);
                 if (found && lane == 0)
                     atomicMax(&bestb, (unsigned int)found);
             }
@@ -499,7 +628,7 @@ __device__ __forceinline__ void search_chunk(const FileTab &t, uint64_t w, uint6
     for (uint64_t k = 0;; k++) {
         const uint64_t b = c0 + (k * NWS + wid) * SB;
         if (b < lim) {
-            const uint64_t found = scan_block<true, SU, NOA1, true>(f, len, b, c0, lim, lane);
+            const uint64_t found = scan_block<true, SU, NOA1, true>(f, len, b, c0, lim, lane); // rare pass
             if (found != NONE && lane == 0)
                 atomicMin(&bestf, (unsigned long long)found);
         }
@@ -541,7 +670,7 @@ __global__ __launch_bounds__(64) void walk_spec_kernel(FileTab t, const uint64_t
         return;
     const uint32_t fi = (uint32_t)(w / t.cpf), c = (uint32_t)(w % t.cpf);
     const uint64_t len = t.file_len[fi];
-    const uint64_t cend = ((uint64_t)c + 1) << t.lg;
+    const uint64_t cend = chunk_edge(t, fi, (uint64_t)c + 1);
     uint32_t count;
     uint64_t exit;
     int32_t st;
@@ -617,7 +746,7 @@ __device__ __forceinline__ uint32_t chain_window(const FileTab &t, uint64_t w, u
     const uint32_t fi = (uint32_t)(w / t.cpf), c = (uint32_t)(w % t.cpf);
     const uint64_t len = t.file_len[fi];
     const uint8_t *f = t.image + t.file_off[fi];
-    const uint64_t cend = ((uint64_t)c + 1) << t.lg;
+    const uint64_t cend = chunk_edge(t, fi, (uint64_t)c + 1);
     RecSlot *sl = slots + w * kcap;
     uint32_t count = 0;
     int32_t st = ST_CONTINUE;
@@ -734,7 +863,7 @@ __device__ __forceinline__ uint32_t chain_wide(const FileTab &t, uint64_t w, uin
     const uint32_t fi = (uint32_t)(w / t.cpf), c = (uint32_t)(w % t.cpf);
     const uint64_t len = t.file_len[fi];
     const uint8_t *f = t.image + t.file_off[fi];
-    const uint64_t cend = ((uint64_t)c + 1) << t.lg;
+    const uint64_t cend = chunk_edge(t, fi, (uint64_t)c + 1);
     RecSlot *sl = slots + w * kcap;
     uint32_t count = 0;
     int32_t st = ST_CONTINUE;
@@ -814,14 +943,14 @@ __global__ __launch_bounds__(64) void walk_spec_win_kernel(FileTab t, const uint
 // instead of following all of them
 // STAMP (diagnostic library): per chunk, s_memrealtime (100 MHz) at the
 // start, after the search and after the chain, and the chain's window loads
-template <int NT, int SU, int MW, uint32_t WB = 0, bool STAMP = false>
+template <int NT, int SU, int MW, uint32_t WB = 0, bool STAMP = false, bool ILP = SEARCH_ILP>
 __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MW))) void walk_search_chain_kernel(
     FileTab t, uint64_t *__restrict__ s_start, int32_t *__restrict__ s_status, uint64_t *__restrict__ s_exit,
     uint32_t *__restrict__ s_count, RecSlot *__restrict__ slots, uint32_t kcap, uint64_t *__restrict__ stamps) {
     const uint64_t t0 = STAMP ? __builtin_amdgcn_s_memrealtime() : 0;
     uint64_t start;
     int32_t status;
-    search_chunk<NT, SU, true>(t, blockIdx.x, start, status);
+    search_chunk<NT, SU, true, ILP>(t, blockIdx.x, start, status);
     if (threadIdx.x == 0) {
         s_start[blockIdx.x] = start;
         s_status[blockIdx.x] = status;
@@ -874,7 +1003,7 @@ __device__ __forceinline__ void stitch_file(const FileTab &t, uint32_t fi, const
     }
     for (uint32_t c = 0; c < t.cpf; c++) {
         const uint64_t w = w0 + c;
-        const uint64_t cend = ((uint64_t)c + 1) << t.lg;
+        const uint64_t cend = chunk_edge(t, fi, (uint64_t)c + 1);
         chunk_base[w] = total;
         if (st != ST_CONTINUE || pos >= cend) { // walk over, or no record starts in this chunk
             true_start[w] = NONE;
@@ -999,7 +1128,7 @@ __device__ __forceinline__ void stitch_file_wave(const FileTab &t, uint32_t fi, 
         const uint64_t pb_in = shfl64(ex, below ? 63u - (uint32_t)__clzll(below) : lane);
         const uint64_t pb = below ? pb_in : carry_pos;
         const bool dead = carry_dead || (tm & below_mask) != 0;
-        const uint64_t cend = ((uint64_t)c + 1) << t.lg;
+        const uint64_t cend = chunk_edge(t, fi, (uint64_t)c + 1);
         const bool good = !in || dead || (act ? ss == pb : pb >= cend);
         if (__ballot(!good)) {
             ok = false;
@@ -1132,7 +1261,7 @@ __device__ __forceinline__ void emit_chunk(const FileTab &t, uint64_t w, const u
     if (w >= (uint64_t)t.nfiles * t.cpf || chunk_mode[w] != MODE_WALK)
         return;
     const uint32_t fi = (uint32_t)(w / t.cpf), c = (uint32_t)(w % t.cpf);
-    const uint64_t cend = ((uint64_t)c + 1) << t.lg;
+    const uint64_t cend = chunk_edge(t, fi, (uint64_t)c + 1);
     const uint64_t foff = t.file_off[fi];
     uint32_t count;
     uint64_t exit;
@@ -1195,6 +1324,30 @@ uint32_t chain_wb() {
         g_chain_wb = e ? std::atoi(e) : (int)CHAIN_WB;
     }
     return (uint32_t)g_chain_wb;
+}
+
+bool search_ilp() { // A/B: ZDBCRC_SEARCH_ILP=0/1 (the fused walk's search filter shape)
+    static const bool v = [] {
+        const char *e = std::getenv("ZDBCRC_SEARCH_ILP");
+        return e ? std::atoi(e) == 1 : SEARCH_ILP;
+    }();
+    return v;
+}
+
+int search_ilp_mw() {
+    static const int v = [] {
+        const char *e = std::getenv("ZDBCRC_SEARCH_ILP_MW");
+        return e ? std::atoi(e) : 6;
+    }();
+    return v;
+}
+
+bool chunk_skew() { // A/B: ZDBCRC_CHUNK_SKEW=0/1
+    static const bool v = [] {
+        const char *e = std::getenv("ZDBCRC_CHUNK_SKEW");
+        return e ? std::atoi(e) == 1 : CHUNK_SKEW;
+    }();
+    return v;
 }
 
 bool serial_stitch() { // A/B: ZDBCRC_SERIAL_STITCH=1 -> one thread per file (the round-2 stitch)
@@ -1292,7 +1445,11 @@ int zdb_datafile_walk_device(const uint8_t *d_image, const uint64_t *d_file_off,
     RecSlot *slots = reinterpret_cast<RecSlot *>(b + 4 * al(nchunks * 8) + 3 * al(nchunks * 4));
     uint32_t *done = reinterpret_cast<uint32_t *>(b + ws.bytes - 256);
 
-    const FileTab t{d_image, d_file_off, d_file_len, nfiles, (uint32_t)cpf64, lg};
+#ifdef ZDBCRC_DIAG
+    const FileTab t{d_image, d_file_off, d_file_len, nfiles, (uint32_t)cpf64, lg, chunk_skew() ? 1u : 0u};
+#else
+    const FileTab t{d_image, d_file_off, d_file_len, nfiles, (uint32_t)cpf64, lg, CHUNK_SKEW ? 1u : 0u};
+#endif
 #ifdef ZDBCRC_DIAG
     const uint32_t cpw = chains_per_wave();
 #else
@@ -1318,7 +1475,20 @@ int zdb_datafile_walk_device(const uint8_t *d_image, const uint64_t *d_file_off,
     hipLaunchKernelGGL((walk_search_chain_kernel<SEARCH_T, SEARCH_SU, SEARCH_MW, WBV, true>),                          \
                        dim3((uint32_t)nchunks), dim3(SEARCH_T), 0, st, t, s_start, s_status, s_exit, s_count, slots,   \
                        kcap, g_stamps)
-        if (g_stamps && nchunks <= g_stamps_n) {
+        if (search_ilp() != SEARCH_ILP) {
+            if (search_ilp_mw() == 5)
+                hipLaunchKernelGGL((walk_search_chain_kernel<SEARCH_T, SEARCH_SU, 5, 0, false, !SEARCH_ILP>),
+                                   dim3((uint32_t)nchunks), dim3(SEARCH_T), 0, st, t, s_start, s_status, s_exit,
+                                   s_count, slots, kcap, nullptr);
+            else if (wb == 2048)
+                hipLaunchKernelGGL((walk_search_chain_kernel<SEARCH_T, SEARCH_SU, SEARCH_MW, 2048, false, !SEARCH_ILP>),
+                                   dim3((uint32_t)nchunks), dim3(SEARCH_T), 0, st, t, s_start, s_status, s_exit,
+                                   s_count, slots, kcap, nullptr);
+            else
+                hipLaunchKernelGGL((walk_search_chain_kernel<SEARCH_T, SEARCH_SU, SEARCH_MW, 0, false, !SEARCH_ILP>),
+                                   dim3((uint32_t)nchunks), dim3(SEARCH_T), 0, st, t, s_start, s_status, s_exit,
+                                   s_count, slots, kcap, nullptr);
+        } else if (g_stamps && nchunks <= g_stamps_n) {
             g_stamps_used = nchunks;
             if (wb == 2048)
                 ZDBCRC_FUSED_STAMP(2048);
@@ -1330,10 +1500,10 @@ int zdb_datafile_walk_device(const uint8_t *d_image, const uint64_t *d_file_off,
         switch (wb) {
 #ifdef ZDBCRC_DIAG
         case 1024: ZDBCRC_FUSED(1024); break;
-        case 2048: ZDBCRC_FUSED(2048); break;
+        case 4096: ZDBCRC_FUSED(4096); break;
         case 8192: ZDBCRC_FUSED(8192); break;
 #endif
-        case 4096: ZDBCRC_FUSED(4096); break;
+        case 2048: ZDBCRC_FUSED(2048); break;
         default: ZDBCRC_FUSED(0); break;
         }
 #undef ZDBCRC_FUSED

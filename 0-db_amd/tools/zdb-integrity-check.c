@@ -246,6 +246,8 @@ typedef struct {
     int (*stream_append)(zdb_crc32_stream_t *, const uint8_t *, size_t);
     int (*stream_checksum)(zdb_crc32_stream_t *, const uint64_t *, const uint32_t *, uint32_t *, size_t);
     void (*stream_close)(zdb_crc32_stream_t *);
+    int (*host_register)(void *, size_t); /* optional: pinned reads (f1) */
+    void (*host_unregister)(void *);
 } gpu_api_t;
 
 static gpu_api_t g_gpu;
@@ -255,6 +257,7 @@ static int g_gpu_devices = 0; /* devices the workers are spread over */
 static pthread_mutex_t g_gpu_mu = PTHREAD_MUTEX_INITIALIZER;
 static pthread_cond_t g_gpu_cv = PTHREAD_COND_INITIALIZER;
 static double g_gpu_t0, g_gpu_t_count, g_gpu_t_up; /* start-up thread timeline (--trace) */
+static double g_t_main;                            /* process timeline origin (--trace) */
 
 #define ENGINE_CPU 0
 #define ENGINE_HIP 1
@@ -309,6 +312,10 @@ static int load_gpu(void) {
     g_gpu.stream_checksum = (int (*)(zdb_crc32_stream_t *, const uint64_t *, const uint32_t *, uint32_t *,
                                      size_t))dlsym(h, "zdb_crc32_stream_checksum");
     g_gpu.stream_close = (void (*)(zdb_crc32_stream_t *))dlsym(h, "zdb_crc32_stream_close");
+    g_gpu.host_register = (int (*)(void *, size_t))dlsym(h, "zdb_crc32_host_register");
+    g_gpu.host_unregister = (void (*)(void *))dlsym(h, "zdb_crc32_host_unregister");
+    if (!g_gpu.host_register || !g_gpu.host_unregister)
+        g_gpu.host_register = NULL;
     if (!g_gpu.batch || !g_gpu.strerror || !g_gpu.device_count || !g_gpu.use_device || !g_gpu.stream_open ||
         !g_gpu.stream_begin || !g_gpu.stream_append || !g_gpu.stream_checksum || !g_gpu.stream_close)
         return 0;
@@ -368,6 +375,8 @@ typedef struct {
     int device;        /* -1 until the thread has bound its GPU               */
     uint8_t *buf;      /* file image, reused from file to file                */
     size_t cap;
+    int pinned;        /* buf is registered with the GPU runtime: reads land
+                          in DMA-able memory and stream appends are direct  */
     zdb_crc32_stream_t *stream; /* this worker's device image + pinned ring   */
 } worker_t;
 
@@ -378,6 +387,10 @@ typedef struct {
 static uint8_t *worker_buffer(worker_t *w, size_t size) {
     if (w->cap >= size)
         return w->buf;
+    if (w->pinned) {
+        g_gpu.host_unregister(w->buf);
+        w->pinned = 0;
+    }
     if (w->buf)
         munmap(w->buf, w->cap);
     const size_t huge = 2u << 20;
@@ -412,6 +425,18 @@ static int worker_stream(worker_t *w, report_t *r) {
         return 0;
     }
     return 1;
+}
+
+/* pin the worker's file buffer in place once the GPU is up (f1): the next
+ * reads land in DMA-able memory and every appended chunk is one direct H2D
+ * copy, overlapping the read of the next chunk -- no staging copy.  Failure
+ * only leaves the staged path. */
+static void worker_pin(worker_t *w, report_t *r, double *pin_ms) {
+    if (w->pinned || !w->buf || !g_gpu.host_register || !worker_stream(w, r))
+        return;
+    const double t0 = now_s();
+    w->pinned = g_gpu.host_register(w->buf, w->cap) == 0;
+    *pin_ms += (now_s() - t0) * 1e3;
 }
 
 /* ---- one datafile, as one reference run would report it ---------------- */
@@ -502,6 +527,7 @@ static void check_file(const config_t *cfg, worker_t *w, const char *filename, r
     const double t_read = now_s();
     size_t len = 0, sent = 0;
     int read_errno = 0, streaming = 0, gpu_failed = 0;
+    double pin_ms = 0;
     uint8_t *image = NULL;
     size_t size = 0;
     if (fstat(fd, &sb) != 0) {
@@ -510,6 +536,8 @@ static void check_file(const config_t *cfg, worker_t *w, const char *filename, r
         read_errno = ENOMEM;
     } else {
         size = (size_t)sb.st_size;
+        if (cfg->engine != ENGINE_CPU && gpu_state(0) == 1)
+            worker_pin(w, r, &pin_ms);
         while (len < size) {
             ssize_t got = pread(fd, image + len, size - len > READ_CHUNK ? READ_CHUNK : size - len, (off_t)len);
             if (got < 0) {
@@ -520,10 +548,12 @@ static void check_file(const config_t *cfg, worker_t *w, const char *filename, r
                 break;
             len += (size_t)got;
             if (cfg->engine != ENGINE_CPU && !streaming && !gpu_failed && gpu_state(0) == 1) {
-                if (worker_stream(w, r) && g_gpu.stream_begin(w->stream, size) == 0)
+                if (worker_stream(w, r) && g_gpu.stream_begin(w->stream, size) == 0) {
                     streaming = 1;
-                else
+                    worker_pin(w, r, &pin_ms); /* the GPU came up during this file */
+                } else {
                     gpu_failed = 1;
+                }
             }
             if (streaming) {
                 if (g_gpu.stream_append(w->stream, image + sent, len - sent) != 0) {
@@ -580,6 +610,7 @@ static void check_file(const config_t *cfg, worker_t *w, const char *filename, r
             if (gpu_failed || !worker_stream(w, r)) {
                 rc = ZDB_CRC32_ELAUNCH;
             } else if (!streaming) {
+                worker_pin(w, r, &pin_ms); /* read before the GPU was up: pinned in place, one DMA */
                 rc = g_gpu.stream_begin(w->stream, len);
                 if (!rc)
                     rc = g_gpu.stream_append(w->stream, image, len);
@@ -657,10 +688,12 @@ static void check_file(const config_t *cfg, worker_t *w, const char *filename, r
     r->status = errors;
     if (cfg->trace)
         fprintf(stderr,
-                "[trace] %s: %zu B, engine %s, read %.2f ms, walk %.2f ms, checksum %.2f ms (of which waiting for the "
-                "GPU start-up %.2f ms), format %.2f ms\n",
-                filename, len, engine_used, (t_walk - t_read) * 1e3, (t_sum - t_walk) * 1e3, (t_fmt - t_sum) * 1e3,
-                gpu_wait_ms, (now_s() - t_fmt) * 1e3);
+                "[trace] %s: %zu B, engine %s, worker %d, %.1f..%.1f ms, read %.2f ms (streamed: %s, buffer pinned: "
+                "%s, pinning %.2f ms), walk %.2f ms, checksum %.2f ms (of which waiting for the GPU start-up %.2f "
+                "ms), format %.2f ms\n",
+                filename, len, engine_used, w->id, (t_read - g_t_main) * 1e3, (now_s() - g_t_main) * 1e3,
+                (t_walk - t_read) * 1e3, streaming ? "yes" : "no", w->pinned ? "yes" : "no", pin_ms,
+                (t_sum - t_walk) * 1e3, (t_fmt - t_sum) * 1e3, gpu_wait_ms, (now_s() - t_fmt) * 1e3);
 out:
     free(recs);
     free(offs);
@@ -704,10 +737,11 @@ static void *worker_main(void *p) {
         pthread_cond_broadcast(&s->cv);
         pthread_mutex_unlock(&s->mu);
     }
-    if (a->w.buf)
+    /* a worker that used the GPU leaves its stream, pinned buffer and
+     * device image to the process's end: main ends GPU runs with _exit, and
+     * unpinning or freeing ~300 MiB per worker would only delay that */
+    if (a->w.buf && !a->w.stream && !a->w.pinned)
         munmap(a->w.buf, a->w.cap);
-    if (a->w.stream)
-        g_gpu.stream_close(a->w.stream);
     return NULL;
 }
 
@@ -717,6 +751,7 @@ static void usage(const char *prog) {
 }
 
 int main(int argc, char *argv[]) {
+    g_t_main = now_s();
     config_t cfg = {ENGINE_AUTO, 0, 0, getenv("ZDBCRC_TOOL_TRACE") != NULL, 0};
     int jobs = 0;
     int argi = 1;
@@ -838,8 +873,11 @@ int main(int argc, char *argv[]) {
     if (cfg.trace && cfg.engine != ENGINE_CPU) {
         pthread_mutex_lock(&g_gpu_mu);
         if (g_gpu_ok >= 0 && g_gpu_t0 > 0)
-            fprintf(stderr, "[trace] GPU start-up: library load + device count %.2f ms, first batch %.2f ms\n",
-                    (g_gpu_t_count - g_gpu_t0) * 1e3, (g_gpu_t_up - g_gpu_t_count) * 1e3);
+            fprintf(stderr,
+                    "[trace] GPU start-up: thread at %.1f ms, library load + device count %.2f ms, first batch %.2f "
+                    "ms, up at %.1f ms; reports done at %.1f ms\n",
+                    (g_gpu_t0 - g_t_main) * 1e3, (g_gpu_t_count - g_gpu_t0) * 1e3, (g_gpu_t_up - g_gpu_t_count) * 1e3,
+                    (g_gpu_t_up - g_t_main) * 1e3, (now_s() - g_t_main) * 1e3);
         pthread_mutex_unlock(&g_gpu_mu);
     }
     if (cfg.engine != ENGINE_CPU) {

@@ -106,7 +106,7 @@ EXPORTED = [
     "zdb_crc32_gpu_initialized", "zdb_crc32_batch_device", "zdb_crc32_batch_device_sized",
     "zdb_crc32_verify_device",
     "zdb_crc32_batch", "zdb_crc32_device_count", "zdb_crc32_use_device", "zdb_crc32_host_alloc",
-    "zdb_crc32_host_free", "zdb_crc32_set_timing",
+    "zdb_crc32_host_free", "zdb_crc32_host_register", "zdb_crc32_host_unregister", "zdb_crc32_set_timing",
     "zdb_crc32_kernel_stats", "zdb_synth_fill", "zdb_synth_fill_device", "zdb_synth_zipf_lengths",
     "zdb_datafile_walk", "zdb_datafile_encode_entry", "zdb_datafile_encode_header",
     "zdb_datafile_payloads", "zdb_datafile_encode_batch", "zdb_datafile_check_device",

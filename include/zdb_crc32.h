@@ -127,7 +127,10 @@ zdb_crc32_stream_t *zdb_crc32_stream_open(size_t slot_bytes, int slots);
 /* start a new image of image_bytes (waits for the previous one's copies) */
 int zdb_crc32_stream_begin(zdb_crc32_stream_t *s, size_t image_bytes);
 
-/* append n bytes at the end of the image (EINVAL past image_bytes) */
+/* append n bytes at the end of the image (EINVAL past image_bytes).  A
+ * source inside pinned memory (zdb_crc32_host_alloc, zdb_crc32_host_register)
+ * is copied by one DMA straight from it with no staging copy and no wait: it
+ * must then stay unchanged until the next begin or checksum on the stream. */
 int zdb_crc32_stream_append(zdb_crc32_stream_t *s, const uint8_t *src, size_t n);
 
 /* out[r] = zdb_crc32(image + offsets[r], lengths[r]) over the bytes appended
@@ -149,6 +152,14 @@ int zdb_crc32_use_device(int device);
  * `bytes`; batches over it are zero-copy) */
 void *zdb_crc32_host_alloc(size_t bytes);
 void zdb_crc32_host_free(void *p);
+
+/* pin existing host memory [p, p + bytes) in place (e.g. a reader's
+ * huge-page buffer, so that a datafile is read straight into DMA-able
+ * memory: f1 ingest); batches whose arena lies inside it (16 bytes readable
+ * past the arena) are zero-copy, stream appends from it are direct DMAs.
+ * Unregister before unmapping or reusing the range for anything else. */
+int zdb_crc32_host_register(void *p, size_t bytes);
+void zdb_crc32_host_unregister(void *p);
 
 /* Instrumentation: when enabled, the main kernel of every batched call is
  * bracketed by HIP events on the caller's stream; the accumulated time of

@@ -1,0 +1,43 @@
+#!/usr/bin/env python3
+"""f1 ingest timeline: the integrity-check tool on 8 and 32 copies of a
+256 MiB datafile (65,000 x 4 KiB values, as bench.py's e2e leg) per engine,
+wall time and the tool's ZDBCRC_TOOL_TRACE lines (process-relative times)."""
+import json, os, subprocess, sys, tempfile, time
+from pathlib import Path
+ROOT = Path(__file__).resolve().parents[1]
+sys.path[:0] = [str(ROOT), str(ROOT / "0-db_amd")]
+import numpy as np, zdbcrc
+
+n = 65000
+vals = zdbcrc.synth_fill(n * 4096, 0xC1)
+vo = np.arange(n, dtype=np.uint64) * 4096
+vl = np.full(n, 4096, np.uint32)
+crcs = np.array([zdbcrc.crc32(vals[i * 4096:(i + 1) * 4096]) for i in range(n)], np.uint32)
+keys = [b"k%d" % i for i in range(n)]
+body, _, _ = zdbcrc.encode_batch(keys, vals, vo, vl, crcs, file_offset=28)
+tool = str(ROOT / "0-db_amd/bin/zdb-integrity-check")
+with tempfile.TemporaryDirectory() as td:
+    with open(f"{td}/d0", "wb") as f:
+        f.write(zdbcrc.encode_header(0) + body)
+    files = []
+    for i in range(8):
+        d = f"{td}/ns{i}"
+        os.mkdir(d)
+        os.link(f"{td}/d0", f"{d}/d0")
+        os.symlink("d0", f"{d}/zdb-data-0")
+        files.append(f"{d}/zdb-data-0")
+    fb = 28 + len(body)
+    for nf in (8, 32):
+        fl = (files * 4)[:nf]
+        for eng in sys.argv[1:] or ["hip", "auto", "cpu"]:
+            walls = []
+            for rep in range(3):
+                t0 = time.perf_counter()
+                p = subprocess.run([tool, f"--engine={eng}", "--jobs=8"] + fl, stdout=subprocess.DEVNULL,
+                                   stderr=subprocess.PIPE, env=dict(os.environ, ZDBCRC_TOOL_TRACE="1"), timeout=300)
+                walls.append(time.perf_counter() - t0)
+                assert p.returncode == 0, p.stderr[-400:]
+            tr = [ln for ln in p.stderr.decode().splitlines() if ln.startswith("[trace]")]
+            print(json.dumps({"files": nf, "engine": eng, "wall_s": [round(w, 4) for w in walls],
+                              "gibs_best": round(nf * fb / min(walls) / 2**30, 2),
+                              "trace_last_run": [ln.replace(td, "") for ln in tr if "payloads" not in ln]}), flush=True)

@@ -419,6 +419,30 @@ def test_tool_gpu_256MiB_matches_reference(big_datafile, engine):
     assert err == ref.stderr
     # hip: the GPU did it; auto: one 256 MiB file is below the start-up policy's threshold
     assert engines == (["hip"] if engine == "hip" else ["cpu"])
+    if engine == "hip":  # f1: the file buffer was pinned in place and went over in one direct DMA
+        assert b"buffer pinned: yes" in p.stderr
+
+
+def test_tool_gpu_pinned_streaming_ingest(big_datafile):
+    """f1 ingest: one worker, the same 256 MiB datafile three times -- once the
+    GPU is up, the worker's buffer is pinned in place and every 32 MiB read is
+    streamed to the device as a direct DMA while the next is read (trace:
+    streamed, buffer pinned); the reports are the reference's, three times"""
+    import re
+    path, ref = big_datafile
+    from test_tool_cpu import TOOL
+    p = subprocess.run([str(TOOL), "--engine=hip", "--jobs=1", str(path), str(path), str(path)], capture_output=True,
+                       env=dict(os.environ, TZ="UTC", ZDBCRC_TOOL_TRACE="1"), timeout=120)
+    t = re.compile(rb"\[\s*\d+\.\d{6}\]")
+    err, engines = split_trace(p.stderr)
+    assert p.returncode == 9  # 3 corrupt payloads per file
+    assert t.sub(b"[T]", p.stdout) == t.sub(b"[T]", ref.stdout) * 3
+    assert err == ref.stderr * 3
+    assert engines == ["hip"] * 3
+    files = [ln for ln in p.stderr.decode().splitlines() if ln.startswith("[trace]") and "buffer pinned" in ln]
+    assert len(files) == 3
+    assert all("buffer pinned: yes" in ln for ln in files)
+    assert "streamed: yes" in files[-1]  # the GPU was up before the last file's first read
 
 
 @pytest.fixture(scope="module", params=["max8MiB", "zipf160MiB"])
