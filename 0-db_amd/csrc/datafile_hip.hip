@@ -308,11 +308,16 @@ __device__ __forceinline__ uint64_t chunk_edge(const FileTab &t, uint32_t fi, ui
 // false positives only cost a back-pointer check).
 __device__ __forceinline__ uint32_t haszero(uint32_t x) { return (x - 0x01010101u) & ~x & 0x80808080u; }
 
+// OR1: both byte tests in one zero-byte test -- byte r of (datalength top
+// byte | flags & 0xFC) is zero iff both are (5 VALU per 4 positions instead
+// of 9; haszero's false positives differ, its hits on zero bytes do not)
+constexpr bool FILTER_OR = true;
+template <bool OR1 = FILTER_OR>
 __device__ __forceinline__ void candidates(const uint32_t (&d)[8], uint32_t (&z)[4]) {
 #pragma unroll
     for (int j = 0; j < 4; j++) {
         const uint32_t fl = __builtin_amdgcn_alignbyte(d[j + 4], d[j + 3], 1u); // bytes 4j+13 .. 4j+16
-        z[j] = haszero(d[j + 1]) & haszero(fl & 0xFCFCFCFCu);
+        z[j] = OR1 ? haszero(d[j + 1] | (fl & 0xFCFCFCFCu)) : haszero(d[j + 1]) & haszero(fl & 0xFCFCFCFCu);
     }
 }
 
@@ -331,7 +336,7 @@ __device__ __forceinline__ uint32_t from_next_lane(uint32_t own_next_row0, uint3
 
 // RELAXED: candidates confirmed by forward_ok instead of the back-pointer
 // (and without the `previous` < p test)
-template <bool FWD, int SU, bool NOA1 = false, bool RELAXED = false>
+template <bool FWD, int SU, bool NOA1 = false, bool RELAXED = false, bool OR1 = FILTER_OR>
 __device__ __forceinline__ uint64_t scan_block(const uint8_t *f, uint64_t len, uint64_t b, uint64_t lo, uint64_t hi,
                                                uint32_t lane) {
     uint4 a0[SU], a1[NOA1 ? 1 : SU], tl = make_uint4(~0u, ~0u, ~0u, ~0u);
@@ -376,7 +381,7 @@ __device__ __forceinline__ uint64_t scan_block(const uint8_t *f, uint64_t len, u
         }
         const uint32_t d[8] = {a0[u].x, a0[u].y, a0[u].z, a0[u].w, nx.x, nx.y, nx.z, nx.w};
         uint32_t z[4];
-        candidates(d, z);
+        candidates<OR1>(d, z);
         if (z[0] | z[1] | z[2] | z[3]) { // rare: confirm through the successor's back-pointer
 #pragma unroll
             for (int j = 0; j < 4; j++) {
@@ -1367,6 +1372,74 @@ int search_variant() {
 }
 #endif
 
+#ifdef ZDBCRC_DIAG
+// search-rate probe: every wave scans its own bytes_per_wave of the image
+// with the search filter, no early exit and no barrier (MODE 0: scan_block
+// backward shape, full filter + confirmation; 1: the same loads, no filter;
+// 2: scan_block_ilp; 3: MODE 0 + a workgroup barrier per block, as the search
+// loop has)
+template <int MODE, int SU>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void search_rate_kernel(
+    const uint8_t *__restrict__ img, uint64_t len, uint64_t per_wave, uint32_t *__restrict__ sink) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint64_t w = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const uint64_t b0 = 4096 + w * per_wave;
+    // positions relative to a 256 MiB "file" (the search's `previous` < p
+    // test passes as often as in C4's files)
+    const uint64_t fb = b0 & ~((1ull << 28) - 1);
+    const uint8_t *f = img + fb;
+    uint32_t x = 0;
+    for (uint64_t b = b0; b < b0 + per_wave && b + 1024u * SU + 64 < len; b += 1024u * SU) {
+        if (MODE == 1) {
+            uint4 v[SU];
+#pragma unroll
+            for (int u = 0; u < SU; u++)
+                v[u] = *reinterpret_cast<const uint4 *>(img + b + 1024u * u + 16u * lane);
+#pragma unroll
+            for (int u = 0; u < SU; u++)
+                x ^= v[u].x ^ v[u].y ^ v[u].z ^ v[u].w;
+        } else if (MODE == 2) {
+            x ^= (uint32_t)scan_block_ilp<false, SU>(f, len - fb, b - fb, 28, len - fb, lane);
+        } else if (MODE == 5) { // the other filter shape
+            x ^= (uint32_t)scan_block<false, SU, true, false, !FILTER_OR>(f, len - fb, b - fb, 28, len - fb, lane);
+        } else {
+            x ^= (uint32_t)scan_block<false, SU, true>(f, len - fb, b - fb, 28, len - fb, lane);
+            if (MODE == 3)
+                __syncthreads();
+        }
+    }
+    if (x == 0x12345678u)
+        sink[0] = x;
+}
+
+// zdbcrc_debug_search_rate: ms of one probe launch over grid workgroups
+float search_rate_ms(const uint8_t *d_img, uint64_t len, int mode, uint64_t per_wave, uint32_t grid) {
+    static uint32_t *sink = nullptr;
+    if (!sink && hipMalloc(&sink, 64) != hipSuccess)
+        return -1.f;
+    hipEvent_t e0, e1;
+    hipEventCreate(&e0);
+    hipEventCreate(&e1);
+    hipEventRecord(e0, 0);
+    switch (mode) {
+    case 0: hipLaunchKernelGGL((search_rate_kernel<0, 8>), dim3(grid), dim3(256), 0, 0, d_img, len, per_wave, sink); break;
+    case 1: hipLaunchKernelGGL((search_rate_kernel<1, 8>), dim3(grid), dim3(256), 0, 0, d_img, len, per_wave, sink); break;
+    case 2: hipLaunchKernelGGL((search_rate_kernel<2, 8>), dim3(grid), dim3(256), 0, 0, d_img, len, per_wave, sink); break;
+    case 3: hipLaunchKernelGGL((search_rate_kernel<3, 8>), dim3(grid), dim3(256), 0, 0, d_img, len, per_wave, sink); break;
+    case 4: hipLaunchKernelGGL((search_rate_kernel<0, 4>), dim3(grid), dim3(256), 0, 0, d_img, len, per_wave, sink); break;
+    case 5: hipLaunchKernelGGL((search_rate_kernel<5, 8>), dim3(grid), dim3(256), 0, 0, d_img, len, per_wave, sink); break;
+    default: return -1.f;
+    }
+    hipEventRecord(e1, 0);
+    float ms = -1.f;
+    if (hipEventSynchronize(e1) == hipSuccess)
+        hipEventElapsedTime(&ms, e0, e1);
+    hipEventDestroy(e0);
+    hipEventDestroy(e1);
+    return ms;
+}
+#endif
+
 // per (device, stream) workspace of the walk
 struct WalkWs {
     void *ptr = nullptr;
@@ -1577,6 +1650,10 @@ uint64_t zdbcrc_debug_walk_stamps(uint64_t *d_stamps, uint64_t n) {
     g_stamps_n = d_stamps ? n : 0;
     g_stamps_used = 0;
     return used;
+}
+
+float zdbcrc_debug_search_rate(const uint8_t *d_img, uint64_t len, int mode, uint64_t per_wave, uint32_t grid) {
+    return search_rate_ms(d_img, len, mode, per_wave, grid);
 }
 
 // A/B hook: the chain window of the fused walk (0, 1024, 2048, 4096, 8192)

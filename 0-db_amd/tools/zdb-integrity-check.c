@@ -273,8 +273,11 @@ static double g_t_main;                            /* process timeline origin (-
 #define AUTO_PCIE_GIBS 40.0
 
 #define READ_CHUNK (32u << 20)  /* pread size: one H2D chunk per read */
-#define SLOT_BYTES (8u << 20)   /* pinned staging slot */
+#define SLOT_BYTES (8u << 20)   /* pinned staging slot (when buffers cannot be pinned in place) */
 #define SLOTS 4
+#define SLOT_BYTES_PINNED (1u << 20) /* the ring is only a fallback when buffers are pinned in place */
+#define SLOTS_PINNED 2
+#define MAX_PREPARED 256       /* worker streams the start-up thread opens ahead */
 
 static double now_s(void) {
     struct timespec t;
@@ -323,11 +326,35 @@ static int load_gpu(void) {
     return g_gpu_count > 0;
 }
 
+/* what the start-up thread prepares besides the devices */
+typedef struct {
+    int gpus;        /* --gpus */
+    int jobs;        /* worker threads */
+    size_t max_file; /* largest file of the scan (device image size) */
+} gpu_prep_t;
+
+static int g_pin_off = -1; /* ZDBCRC_TOOL_PIN=0: no in-place pinning (measurement A/B) */
+static int pin_off(void) {
+    if (g_pin_off < 0) {
+        const char *e = getenv("ZDBCRC_TOOL_PIN");
+        g_pin_off = e && e[0] == '0';
+    }
+    return g_pin_off;
+}
+
+static zdb_crc32_stream_t *g_pre_stream[MAX_PREPARED]; /* worker j's ingest stream, opened ahead */
+static double g_gpu_t_dev;                             /* devices up (before the streams) */
+
 /* the GPU start-up thread: load the library, bring every device the workers
- * will use up (code object, tables, workspace: one tiny batch each) while the
- * workers read their files */
+ * will use up (code object, tables, workspace: one tiny batch each), then
+ * open every worker's ingest stream with its device image sized for the
+ * largest file -- while the workers read their first files, so that a worker
+ * that finds the GPU up only pins its buffer and copies (the eight workers'
+ * stream set-up otherwise contends in the runtime right when the GPU comes up:
+ * 70-160 ms per worker, profiles/r3/tool_timeline.jsonl) */
 static void *gpu_init_main(void *arg) {
-    const int want = *(const int *)arg;
+    const gpu_prep_t *prep = (const gpu_prep_t *)arg;
+    const int want = prep->gpus;
     g_gpu_t0 = now_s();
     int ok = load_gpu();
     g_gpu_t_count = now_s();
@@ -339,6 +366,18 @@ static void *gpu_init_main(void *arg) {
             uint32_t l = 64, c = 0;
             ok = g_gpu.use_device(d) == 0 && g_gpu.batch(b, sizeof(b), &o, &l, &c, 1) == 0;
         }
+    }
+    g_gpu_t_dev = now_s();
+    const int pinned = g_gpu.host_register && !pin_off();
+    for (int j = 0; ok && j < prep->jobs && j < MAX_PREPARED; j++) {
+        if (g_gpu.use_device(j % g_gpu_devices) != 0)
+            break;
+        zdb_crc32_stream_t *st = g_gpu.stream_open(pinned ? SLOT_BYTES_PINNED : SLOT_BYTES, pinned ? SLOTS_PINNED : SLOTS);
+        if (st && prep->max_file && g_gpu.stream_begin(st, prep->max_file) != 0) {
+            g_gpu.stream_close(st);
+            st = NULL;
+        }
+        g_pre_stream[j] = st; /* NULL: the worker opens its own */
     }
     pthread_mutex_lock(&g_gpu_mu);
     g_gpu_t_up = now_s();
@@ -411,6 +450,14 @@ static uint8_t *worker_buffer(worker_t *w, size_t size) {
 static int worker_stream(worker_t *w, report_t *r) {
     if (w->stream)
         return 1;
+    if (w->device < 0 && w->id < MAX_PREPARED && g_pre_stream[w->id]) { /* opened by the start-up thread */
+        w->device = w->id % g_gpu_devices;
+        if (g_gpu.use_device(w->device) == 0) {
+            w->stream = g_pre_stream[w->id];
+            g_pre_stream[w->id] = NULL;
+            return 1;
+        }
+    }
     if (w->device < 0) {
         w->device = w->id % g_gpu_devices;
         int rc = g_gpu.use_device(w->device);
@@ -419,7 +466,8 @@ static int worker_stream(worker_t *w, report_t *r) {
             return 0;
         }
     }
-    w->stream = g_gpu.stream_open(SLOT_BYTES, SLOTS);
+    const int pinned = g_gpu.host_register && !pin_off();
+    w->stream = g_gpu.stream_open(pinned ? SLOT_BYTES_PINNED : SLOT_BYTES, pinned ? SLOTS_PINNED : SLOTS);
     if (!w->stream) {
         rep_err(r, "[-] zdb-integrity-check: GPU %d: cannot open an ingest stream (use --engine=cpu)\n", w->device);
         return 0;
@@ -432,7 +480,7 @@ static int worker_stream(worker_t *w, report_t *r) {
  * copy, overlapping the read of the next chunk -- no staging copy.  Failure
  * only leaves the staged path. */
 static void worker_pin(worker_t *w, report_t *r, double *pin_ms) {
-    if (w->pinned || !w->buf || !g_gpu.host_register || !worker_stream(w, r))
+    if (pin_off() || w->pinned || !w->buf || !g_gpu.host_register || !worker_stream(w, r))
         return;
     const double t0 = now_s();
     w->pinned = g_gpu.host_register(w->buf, w->cap) == 0;
@@ -804,9 +852,17 @@ int main(int argc, char *argv[]) {
 
     /* GPU start-up overlaps the reads (the thread is never joined: a
      * worker that needs the GPU waits for it; exit does not) */
+    static gpu_prep_t prep;
+    prep.gpus = cfg.gpus;
+    prep.jobs = njobs;
+    for (int i = argi; i < argc; i++) {
+        struct stat fst;
+        if (stat(argv[i], &fst) == 0 && (size_t)fst.st_size > prep.max_file)
+            prep.max_file = (size_t)fst.st_size;
+    }
     if (cfg.engine == ENGINE_HIP || (cfg.engine == ENGINE_AUTO && g_gpu_ok != 0)) {
         pthread_t gt;
-        if (pthread_create(&gt, NULL, gpu_init_main, &cfg.gpus) != 0)
+        if (pthread_create(&gt, NULL, gpu_init_main, &prep) != 0)
             g_gpu_ok = 0;
         else
             pthread_detach(gt);
@@ -875,9 +931,9 @@ int main(int argc, char *argv[]) {
         if (g_gpu_ok >= 0 && g_gpu_t0 > 0)
             fprintf(stderr,
                     "[trace] GPU start-up: thread at %.1f ms, library load + device count %.2f ms, first batch %.2f "
-                    "ms, up at %.1f ms; reports done at %.1f ms\n",
-                    (g_gpu_t0 - g_t_main) * 1e3, (g_gpu_t_count - g_gpu_t0) * 1e3, (g_gpu_t_up - g_gpu_t_count) * 1e3,
-                    (g_gpu_t_up - g_t_main) * 1e3, (now_s() - g_t_main) * 1e3);
+                    "ms, worker streams %.2f ms, up at %.1f ms; reports done at %.1f ms\n",
+                    (g_gpu_t0 - g_t_main) * 1e3, (g_gpu_t_count - g_gpu_t0) * 1e3, (g_gpu_t_dev - g_gpu_t_count) * 1e3,
+                    (g_gpu_t_up - g_gpu_t_dev) * 1e3, (g_gpu_t_up - g_t_main) * 1e3, (now_s() - g_t_main) * 1e3);
         pthread_mutex_unlock(&g_gpu_mu);
     }
     if (cfg.engine != ENGINE_CPU) {

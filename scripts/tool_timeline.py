@@ -30,14 +30,16 @@ with tempfile.TemporaryDirectory() as td:
     for nf in (8, 32):
         fl = (files * 4)[:nf]
         for eng in sys.argv[1:] or ["hip", "auto", "cpu"]:
+          for pin in (("1", "0") if eng == "hip" else ("1",)):
             walls = []
             for rep in range(3):
                 t0 = time.perf_counter()
                 p = subprocess.run([tool, f"--engine={eng}", "--jobs=8"] + fl, stdout=subprocess.DEVNULL,
-                                   stderr=subprocess.PIPE, env=dict(os.environ, ZDBCRC_TOOL_TRACE="1"), timeout=300)
+                                   stderr=subprocess.PIPE, env=dict(os.environ, ZDBCRC_TOOL_TRACE="1",
+                                                                    ZDBCRC_TOOL_PIN=pin), timeout=300)
                 walls.append(time.perf_counter() - t0)
                 assert p.returncode == 0, p.stderr[-400:]
             tr = [ln for ln in p.stderr.decode().splitlines() if ln.startswith("[trace]")]
-            print(json.dumps({"files": nf, "engine": eng, "wall_s": [round(w, 4) for w in walls],
+            print(json.dumps({"files": nf, "engine": eng, "pin": pin, "wall_s": [round(w, 4) for w in walls],
                               "gibs_best": round(nf * fb / min(walls) / 2**30, 2),
                               "trace_last_run": [ln.replace(td, "") for ln in tr if "payloads" not in ln]}), flush=True)
