@@ -47,6 +47,7 @@
 #include <cstring>
 #include <map>
 #include <mutex>
+#include <tuple>
 
 #include <hip/hip_runtime.h>
 
@@ -1440,6 +1441,59 @@ float search_rate_ms(const uint8_t *d_img, uint64_t len, int mode, uint64_t per_
 }
 #endif
 
+// default chunk size, from the record density of the store: one wave per
+// file walks the headers of its first DENSITY_SAMPLE bytes through 4 KiB LDS
+// windows (records that start there, and the bytes they cover, summed over
+// the files).  A chunk's chain has one dependent round trip per record that
+// does not share a window with the one before it, so a store of small values
+// (4 KiB: ~2,000 records per 8 MiB chunk) needs smaller chunks, while C4's
+// Zipf mix (~170 records per 8 MiB, most bytes in long values that every
+// chunk start has to search across) needs large ones.
+constexpr uint32_t DENSITY_SAMPLE = 64u << 10;
+constexpr uint32_t DENSITY_MAX_PER_CHUNK = 512; // records per default chunk before it is made smaller
+constexpr uint32_t DENSITY_TARGET = 128;        // records per chunk when it is
+constexpr uint32_t MIN_LG_CHUNK = 16;
+
+__global__ __launch_bounds__(64) void walk_density_kernel(FileTab t, unsigned long long *__restrict__ acc) {
+    __shared__ __attribute__((aligned(16))) uint32_t lds[4096 / 4 + 4];
+    const uint32_t fi = blockIdx.x, lane = threadIdx.x;
+    const uint64_t len = t.file_len[fi];
+    const uint8_t *f = t.image + t.file_off[fi];
+    const uint64_t lim = len < DENSITY_SAMPLE + ZDB_DATA_HEADER_SIZE ? len : DENSITY_SAMPLE + ZDB_DATA_HEADER_SIZE;
+    uint64_t pos = ZDB_DATA_HEADER_SIZE;
+    uint32_t count = 0;
+    WideWindow<4096> win;
+    win.base = 0;
+    bool have = false;
+    while (pos < lim && pos + ZDB_ENTRY_HEADER_SIZE <= len) {
+        if (!have || reinterpret_cast<uintptr_t>(f + pos) - win.base + 13u > 4096u) {
+            load_wide<4096>(win, f, len, pos, lane);
+            stage_wide<4096>(win, lds, lane);
+            have = true;
+        }
+        const Hdr h = lds_hdr(lds, (uint32_t)(reinterpret_cast<uintptr_t>(f + pos) - win.base));
+        const uint64_t next = pos + ZDB_ENTRY_HEADER_SIZE + h.idl + h.L;
+        if (next > len)
+            break;
+        count++;
+        pos = next;
+    }
+    if (lane == 0 && count) {
+        atomicAdd(acc, (unsigned long long)count);
+        atomicAdd(acc + 1, (unsigned long long)(pos - ZDB_DATA_HEADER_SIZE));
+    }
+}
+
+struct DensityKey {
+    const uint8_t *image;
+    const uint64_t *file_off;
+    uint32_t nfiles;
+    uint64_t max_file_len;
+    bool operator<(const DensityKey &o) const {
+        return std::tie(image, file_off, nfiles, max_file_len) < std::tie(o.image, o.file_off, o.nfiles, o.max_file_len);
+    }
+};
+
 // per (device, stream) workspace of the walk
 struct WalkWs {
     void *ptr = nullptr;
@@ -1447,6 +1501,11 @@ struct WalkWs {
 };
 std::mutex g_walk_mu[64];
 std::map<void *, WalkWs> g_walk_ws[64];
+// the default chunk size chosen for a store, by its image and file table
+// (any chunk size gives the same walk: a stale entry after the same buffers
+// are refilled with another store only costs time)
+std::map<DensityKey, uint32_t> g_walk_lg[64];
+unsigned long long *g_density_acc[64];
 
 } // namespace
 
@@ -1471,6 +1530,39 @@ int zdb_datafile_walk_device(const uint8_t *d_image, const uint64_t *d_file_off,
     }
     if (max_file_len > (1ull << 32)) // datafile offsets are u32 (data.h:59, index.h:54)
         return ZDB_CRC32_EINVAL;
+    zdbcrc_internal_mark_hip();
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64)
+        return ZDB_CRC32_ENODEV;
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    std::lock_guard<std::mutex> g(g_walk_mu[dev]);
+    if (!chunk_bytes) { // the store's own default (walk_density_kernel), measured once per store
+        const DensityKey key{d_image, d_file_off, nfiles, max_file_len};
+        auto it = g_walk_lg[dev].find(key);
+        if (it != g_walk_lg[dev].end()) {
+            lg = it->second;
+        } else {
+            if (!g_density_acc[dev] && hipMalloc(&g_density_acc[dev], 2 * sizeof(unsigned long long)) != hipSuccess)
+                return ZDB_CRC32_ENOMEM;
+            unsigned long long h[2] = {0, 0};
+            const FileTab t0{d_image, d_file_off, d_file_len, nfiles, 1, DEFAULT_LG_CHUNK, 0};
+            if (hipMemsetAsync(g_density_acc[dev], 0, sizeof(h), st) != hipSuccess)
+                return ZDB_CRC32_ELAUNCH;
+            hipLaunchKernelGGL(walk_density_kernel, dim3(nfiles), dim3(64), 0, st, t0, g_density_acc[dev]);
+            if (hipGetLastError() != hipSuccess ||
+                hipMemcpyAsync(h, g_density_acc[dev], sizeof(h), hipMemcpyDeviceToHost, st) != hipSuccess ||
+                hipStreamSynchronize(st) != hipSuccess)
+                return ZDB_CRC32_ELAUNCH;
+            // records per default chunk = count / bytes * 2^23
+            if (h[0] && h[1] && (double)h[0] * (double)(1ull << DEFAULT_LG_CHUNK) >
+                                     (double)DENSITY_MAX_PER_CHUNK * (double)h[1]) {
+                const double c = (double)DENSITY_TARGET * (double)h[1] / (double)h[0]; // bytes per target chunk
+                while (lg > MIN_LG_CHUNK && (double)(1ull << lg) > c)
+                    lg--;
+            }
+            g_walk_lg[dev][key] = lg;
+        }
+    }
     const uint64_t cpf64 = max_file_len ? (max_file_len + (1ull << lg) - 1) >> lg : 1;
     const uint64_t nchunks = cpf64 * nfiles;
     // one search workgroup of SEARCH_T threads per chunk and up to 512 slot
@@ -1478,12 +1570,6 @@ int zdb_datafile_walk_device(const uint8_t *d_image, const uint64_t *d_file_off,
     // an oversized store fails here and not as a late launch error
     if (nchunks >= (1ull << 32) / SEARCH_T || nchunks * (nchunks <= 65536 ? 512u : 64u) >= (1ull << 32))
         return ZDB_CRC32_EINVAL;
-    zdbcrc_internal_mark_hip();
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64)
-        return ZDB_CRC32_ENODEV;
-    hipStream_t st = static_cast<hipStream_t>(stream);
-    std::lock_guard<std::mutex> g(g_walk_mu[dev]);
     // workspace: per chunk s_start, s_exit, true_start, chunk_base (u64),
     // s_count, s_status, chunk_mode (4 B), kcap record slots (16 B each)
     const uint32_t kcap = nchunks <= 65536 ? 512u : 64u;

@@ -31,15 +31,22 @@ with tempfile.TemporaryDirectory() as td:
         fl = (files * 4)[:nf]
         for eng in sys.argv[1:] or ["hip", "auto", "cpu"]:
           for pin in (("1", "0") if eng == "hip" else ("1",)):
-            walls = []
-            for rep in range(3):
+            walls, runs = [], []
+            for rep in range(5):
                 t0 = time.perf_counter()
                 p = subprocess.run([tool, f"--engine={eng}", "--jobs=8"] + fl, stdout=subprocess.DEVNULL,
                                    stderr=subprocess.PIPE, env=dict(os.environ, ZDBCRC_TOOL_TRACE="1",
                                                                     ZDBCRC_TOOL_PIN=pin), timeout=300)
                 walls.append(time.perf_counter() - t0)
                 assert p.returncode == 0, p.stderr[-400:]
+                su = [ln for ln in p.stderr.decode().splitlines() if ln.startswith("[trace] GPU start-up")]
+                if su:  # process-relative: GPU up, reports done; the rest of the wall time is process exit
+                    import re
+                    up = float(re.search(r"up at ([\d.]+) ms", su[0]).group(1))
+                    done = float(re.search(r"reports done at ([\d.]+) ms", su[0]).group(1))
+                    runs.append({"wall_ms": round(walls[-1] * 1e3, 1), "gpu_up_ms": up, "reports_done_ms": done,
+                                 "after_reports_ms": round(walls[-1] * 1e3 - done, 1)})
             tr = [ln for ln in p.stderr.decode().splitlines() if ln.startswith("[trace]")]
             print(json.dumps({"files": nf, "engine": eng, "pin": pin, "wall_s": [round(w, 4) for w in walls],
-                              "gibs_best": round(nf * fb / min(walls) / 2**30, 2),
+                              "gibs_best": round(nf * fb / min(walls) / 2**30, 2), "runs": runs,
                               "trace_last_run": [ln.replace(td, "") for ln in tr if "payloads" not in ln]}), flush=True)
