@@ -269,7 +269,7 @@ static double g_t_main;                            /* process timeline origin (-
  * PCIe at AUTO_PCIE_GIBS (DESIGN.md §7.1 measures all three), so the GPU is
  * started only when bytes / (workers * cpu) > start + bytes / pcie. */
 #define AUTO_CPU_GIBS 10.0
-#define AUTO_GPU_START_S 0.25
+#define AUTO_GPU_START_S 0.30 /* HIP start-up 150-340 ms + exit, profiles/r3/tool_timeline.jsonl */
 #define AUTO_PCIE_GIBS 40.0
 
 #define READ_CHUNK (32u << 20)  /* pread size: one H2D chunk per read */

@@ -269,6 +269,41 @@ def test_device_scan_c4_shaped_store(dev):
     assert sorted(st.mismatch[:cnt].cpu().numpy().tolist()) == hit
 
 
+def test_device_scan_small_value_store_default_chunks(dev):
+    """a store of 4 KiB values (C2u-shaped datafiles, 4 x 64 MiB) through the
+    default chunk size -- chosen from the store's record density by the
+    sampling kernel (512 KiB here instead of 8 MiB: ~2,000 dependent hops per
+    chain otherwise) -- and at two fixed sizes: the same entries as the
+    layout, every chunk speculated right, no mismatch; then one flipped byte"""
+    sys.path.insert(0, str(ROOT))
+    import bench
+    files, cap, val = 4, 64 << 20, 4096
+    per = (cap - bench.FILE_HDR) // (bench.ENTRY_HDR + bench.C4_KEY + val)
+    n = per * files
+    step = bench.ENTRY_HDR + bench.C4_KEY + val
+    file_of = np.repeat(np.arange(files), per)
+    rel = bench.FILE_HDR + (np.arange(n) % per) * step
+    fsize = np.full(files, bench.FILE_HDR + per * step, np.int64)
+    file_off = np.concatenate([[0], np.cumsum(fsize[:-1])])
+    entry_off = file_off[file_of] + rel
+    lay = {"lens": np.full(n, val, np.int64), "entry_off": entry_off,
+           "payload_off": entry_off + bench.ENTRY_HDR + bench.C4_KEY,
+           "prev": np.where(np.arange(n) % per == 0, 0, rel - step), "file_of": file_of, "file_off": file_off,
+           "file_size": fsize, "total": int(file_off[-1] + fsize[-1])}
+    img, _, _, _, crcs = bench.c4_build_device(lay, 0x5A11)
+    st = dev.DeviceStore(img, lay["file_off"], lay["file_size"], capacity=n + 10)
+    for chunk in (0, 8 << 20, 256 << 10):
+        assert st.scan(chunk) == n
+        np.testing.assert_array_equal(st.entry_off[:n].cpu().numpy(), lay["entry_off"])
+        assert int(st.mismatch_count.cpu()[0]) == 0
+        assert int(st.rewalks.cpu()[-1]) == 0
+        np.testing.assert_array_equal(st.computed[:n].cpu().numpy().view(np.uint32), crcs)
+    img[int(lay["payload_off"][n // 3]) + 7] ^= 0x10
+    st.scan()
+    cnt = int(st.mismatch_count.cpu()[0])
+    assert st.mismatch[:cnt].cpu().numpy().tolist() == [n // 3]
+
+
 def test_device_scan_files_over_2GiB(dev):
     """two C4-shaped datafiles of ~3 GiB each (entry offsets past 2^31, the
     top of a datafile's u32 offsets in reach): the walk finds exactly the
