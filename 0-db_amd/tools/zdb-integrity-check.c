@@ -268,6 +268,10 @@ static double g_t_main;                            /* process timeline origin (-
  * engine pays AUTO_GPU_START_S of runtime start-up and moves the bytes over
  * PCIe at AUTO_PCIE_GIBS (DESIGN.md §7.1 measures all three), so the GPU is
  * started only when bytes / (workers * cpu) > start + bytes / pcie. */
+/* With J workers the rule can only hold when J * AUTO_CPU_GIBS < AUTO_PCIE_GIBS,
+ * i.e. for at most 3 workers: a scan with 4 or more workers stays on the
+ * scalar engine whatever its size (the host checksums faster than PCIe moves
+ * the bytes). */
 #define AUTO_CPU_GIBS 10.0
 #define AUTO_GPU_START_S 0.30 /* HIP start-up 150-340 ms + exit, profiles/r3/tool_timeline.jsonl */
 #define AUTO_PCIE_GIBS 40.0

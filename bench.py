@@ -514,7 +514,9 @@ def e2e_legs(offs, lens, seed) -> dict:
             files.append(f"{d}/zdb-data-0")
         tool = str(ROOT / "0-db_amd/bin/zdb-integrity-check")
         scan = {"files": len(files), "file_bytes": 28 + len(body)}
-        files32 = files * 4  # 32 files: a store large enough for the GPU start-up to pay off
+        # 32 files (8 GiB): the GPU engine's fixed cost (HIP start-up and exit) spread over more
+        # bytes; `auto` still takes the scalar engine here (J x AUTO_CPU_GIBS >= AUTO_PCIE_GIBS for 8 workers)
+        files32 = files * 4
         runs = {"gpu_tool_jobs8": ([[tool, "--engine=hip", "--jobs=8"] + files], 8),
                 "auto_engine_tool_jobs8": ([[tool, "--engine=auto", "--jobs=8"] + files], 8),
                 "scalar_engine_tool_jobs8": ([[tool, "--engine=cpu", "--jobs=8"] + files], 8),
