@@ -1340,6 +1340,14 @@ bool search_ilp() { // A/B: ZDBCRC_SEARCH_ILP=0/1 (the fused walk's search filte
     return v;
 }
 
+int search_nt() { // A/B: ZDBCRC_SEARCH_NT = 512 / 1024 threads per chunk in the fused walk
+    static const int v = [] {
+        const char *e = std::getenv("ZDBCRC_SEARCH_NT");
+        return e ? std::atoi(e) : SEARCH_T;
+    }();
+    return v;
+}
+
 int search_ilp_mw() {
     static const int v = [] {
         const char *e = std::getenv("ZDBCRC_SEARCH_ILP_MW");
@@ -1634,7 +1642,24 @@ int zdb_datafile_walk_device(const uint8_t *d_image, const uint64_t *d_file_off,
     hipLaunchKernelGGL((walk_search_chain_kernel<SEARCH_T, SEARCH_SU, SEARCH_MW, WBV, true>),                          \
                        dim3((uint32_t)nchunks), dim3(SEARCH_T), 0, st, t, s_start, s_status, s_exit, s_count, slots,   \
                        kcap, g_stamps)
-        if (search_ilp() != SEARCH_ILP) {
+        if (search_nt() == 512 || search_nt() == 1024) { // A/B: more waves per chunk search
+            const bool stamp = g_stamps && nchunks <= g_stamps_n;
+            if (stamp)
+                g_stamps_used = nchunks;
+            uint64_t *sp = stamp ? g_stamps : nullptr;
+            if (search_nt() == 512 && stamp)
+                hipLaunchKernelGGL((walk_search_chain_kernel<512, SEARCH_SU, SEARCH_MW, 2048, true>), dim3((uint32_t)nchunks),
+                                   dim3(512), 0, st, t, s_start, s_status, s_exit, s_count, slots, kcap, sp);
+            else if (search_nt() == 512)
+                hipLaunchKernelGGL((walk_search_chain_kernel<512, SEARCH_SU, SEARCH_MW, 2048, false>), dim3((uint32_t)nchunks),
+                                   dim3(512), 0, st, t, s_start, s_status, s_exit, s_count, slots, kcap, sp);
+            else if (stamp)
+                hipLaunchKernelGGL((walk_search_chain_kernel<1024, SEARCH_SU, SEARCH_MW, 2048, true>), dim3((uint32_t)nchunks),
+                                   dim3(1024), 0, st, t, s_start, s_status, s_exit, s_count, slots, kcap, sp);
+            else
+                hipLaunchKernelGGL((walk_search_chain_kernel<1024, SEARCH_SU, SEARCH_MW, 2048, false>), dim3((uint32_t)nchunks),
+                                   dim3(1024), 0, st, t, s_start, s_status, s_exit, s_count, slots, kcap, sp);
+        } else if (search_ilp() != SEARCH_ILP) {
             if (search_ilp_mw() == 5)
                 hipLaunchKernelGGL((walk_search_chain_kernel<SEARCH_T, SEARCH_SU, 5, 0, false, !SEARCH_ILP>),
                                    dim3((uint32_t)nchunks), dim3(SEARCH_T), 0, st, t, s_start, s_status, s_exit,
