@@ -82,7 +82,11 @@ constexpr uint64_t DYN_MIN_UNITS_PER_WAVE = 4096;
 // record is one same-address atomic XOR: one huge record would serialise them)
 constexpr uint64_t DYN_MAX_CHUNKS_PER_RECORD = 64;
 // records up to this many bytes take the small-record loop shape (PP)
-constexpr uint64_t SMALL_RECORD_MAX = 4096;
+[[maybe_unused]] constexpr uint64_t SMALL_RECORD_MAX = 4096;
+// ... and up to this many the packed kernel (four records per wave): 2.0-2.4x
+// faster than the small shape for records of 64 B - 2 KiB, 3 % slower at
+// 4 KiB (profiles/r3/ab_packed_sizes.jsonl)
+[[maybe_unused]] constexpr uint64_t TINY_RECORD_MAX = 2048;
 // record-relative grids of records this long load from the dword below the
 // record and fold its last bytes in at the end (next_seg_batched): the fold
 // waits for one dword load at the record's end, which small records cannot
@@ -920,7 +924,6 @@ __global__ __launch_bounds__(WGT, WPE) void crc_batch_kernel_v3(
     }
 }
 
-#ifdef ZDBCRC_DIAG // measured, not shipped: profiles/r3/ab_packed_kernel.jsonl
 // ---------------------------------------------------------------------------
 // packed small-record kernel: four records per wave, one per row of 16 lanes
 // ---------------------------------------------------------------------------
@@ -1393,7 +1396,6 @@ __global__ __launch_bounds__(WGT, WPE) void crc_packed_kernel(
         r0 = rb; // range done
     }
 }
-#endif // ZDBCRC_DIAG (packed kernel)
 
 typedef void (*crc_kernel_fn)(const uint8_t *, const uint64_t *, const uint32_t *, PlanArgs, uint64_t,
                               uint32_t *, const uint32_t *, uint32_t, uint32_t *, uint32_t);
@@ -1472,7 +1474,7 @@ constexpr int kNumVariants = (int)(sizeof(kVariants) / sizeof(kVariants[0]));
 std::atomic<int> g_variant{-1};
 std::atomic<int> g_host_mode{0};
 
-const KernelVariant &variant(bool /*small: the A/B harness picks by index*/ = false) {
+const KernelVariant &variant(uint64_t /*max_len: the A/B harness picks by index*/ = 0) {
     int v = g_variant.load();
     if (v < 0) {
         const char *e = std::getenv("ZDBCRC_VARIANT");
@@ -1506,7 +1508,16 @@ const KernelVariant kSmall = {"v3_wg768_nt_dyn4c4p32_sp_pp_wait_bmg_xp",
                               crc_batch_kernel_v3<768, 6, false, 0, UNIT_OVH, false, true, false, 0, 4, 4, 32, true, 3,
                                                   false, true, true>,
                               768};
-const KernelVariant &variant(bool small = false) { return small ? kSmall : kDefault; }
+// batches of records <= 2 KiB: the packed kernel (512 threads: the 768-thread
+// build spills, profiles/r3/ab_packed_kernel.jsonl)
+const KernelVariant kTiny = {"pk_wg512_dyn4c4p32_sp", crc_packed_kernel<512, 4, 4, 4, 32, true, 0>, 512, WG_PER_CU,
+                             UO_PK};
+// the kernel for a batch whose records are at most max_len bytes (0: unknown)
+const KernelVariant &variant(uint64_t max_len = 0) {
+    if (max_len == 0 || max_len > SMALL_RECORD_MAX)
+        return kDefault;
+    return max_len <= TINY_RECORD_MAX ? kTiny : kSmall;
+}
 #endif
 
 // unit count per record: ovh (the variant's per-record charge) + number of
@@ -2212,8 +2223,7 @@ int zdb_crc32_batch_device_sized(const uint8_t *d_arena, const uint64_t *d_offse
     DeviceCtx *c;
     if ((rc = ensure_device(dev, &c)))
         return rc;
-    const bool small = max_length > 0 && max_length <= SMALL_RECORD_MAX;
-    return enqueue_batch(dev, *c, variant(small), d_arena, d_offsets, d_lengths, d_out, n,
+    return enqueue_batch(dev, *c, variant(max_length), d_arena, d_offsets, d_lengths, d_out, n,
                          static_cast<hipStream_t>(stream));
 }
 
@@ -2379,7 +2389,7 @@ int zdb_crc32_batch(const uint8_t *arena, size_t arena_len, const uint64_t *offs
 #else
     const bool mailbox = n <= MAILBOX_RECORDS;
 #endif
-    const KernelVariant &kv = variant(max_len <= SMALL_RECORD_MAX);
+    const KernelVariant &kv = variant(max_len ? max_len : 1); // all empty: any shape
     if (!d_arena)
         d_arena = h.arena;
     const UnitCount uc{d_arena, offsets, lengths, n, kv.unit_ovh};
@@ -2719,7 +2729,7 @@ int zdb_crc32_stream_checksum(zdb_crc32_stream_t *s, const uint64_t *offsets, co
         DeviceCtx *c;
         int rc = ensure_device(s->dev, &c);
         if (!rc)
-            rc = enqueue_batch(s->dev, *c, variant(max_len <= SMALL_RECORD_MAX), s->d_image,
+            rc = enqueue_batch(s->dev, *c, variant(max_len ? max_len : 1), s->d_image,
                                reinterpret_cast<const uint64_t *>(s->d_desc),
                                reinterpret_cast<const uint32_t *>(s->d_desc + n * 8), d_out, n, s->st);
         if (rc)

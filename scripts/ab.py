@@ -65,6 +65,15 @@ for wl in [w for w in work.split(",") if w and w != "none"]:
         lens = np.tile(base, reps)
         lens = lens[:int(np.searchsorted(np.cumsum(lens), size))]
         seed = 0x5A0DB5EED + 3
+    elif wl.startswith("zipf_le"):  # C3's records up to N bytes, tiled to `size`
+        base = zdbcrc.zipf_lengths(4 << 30, 0xC3C3C3).astype(np.int64)
+        base = base[base <= int(wl[7:])]
+        reps = max(1, -(-size // int(base.sum())))
+        lens = np.tile(base, reps)
+        lens = lens[:int(np.searchsorted(np.cumsum(lens), size))]
+        seed = 0x5A0DB5EED + 3
+    elif wl.startswith("fixed") and wl[5:].isdigit():  # fixed N-byte records, packed back to back
+        lens = np.full(size // int(wl[5:]), int(wl[5:]), np.int64); seed = 0x5A0DB5EED
     elif wl == "single":
         lens = np.array([size - 16], np.int64); seed = 0x5A0DB5EED
     elif wl == "fixed64k":

@@ -651,6 +651,65 @@ def test_small_record_shape(dev, oracle_c, case):
     np.testing.assert_array_equal(dev.batch_host(arena, offs.astype(np.uint64), lens.astype(np.uint32)), want)
 
 
+def _packed_cases():
+    """crafted batches for the packed kernel (records <= 2 KiB: four per wave,
+    one per row of 16 lanes; dword-anchored grid, piece 0 shifted up when a
+    record starts in the first 16 bytes of a page)"""
+    rng = np.random.default_rng(5)
+    out = {}
+    lens = np.arange(0, 301)
+    out["every_len_0_300"] = (np.cumsum(np.concatenate([[1], lens[:-1] + 3])), lens, 2048)
+    lens = np.full(64 * 16, 2048)
+    out["2k_every_alignment"] = (np.array([4096 * 2 * i + (i % 64) for i in range(len(lens))]), lens, 2048)
+    offs, ls = [], []
+    for p in range(64):
+        for a in range(16):
+            for L in (1, 2, 3, 5, 17, 100, 2047, 2045):
+                offs.append(4096 * (p * 4 + 1) + a)
+                ls.append(L)
+    out["page_start_records"] = (np.array(offs), np.array(ls), 2048)
+    out["arena_start"] = (np.array([0, 1, 2, 3, 5, 9, 15, 0, 3]), np.array([100, 1, 2, 3, 7, 13, 1, 2048, 2045]), 2048)
+    lens = rng.integers(0, 2049, 200_000)
+    offs = np.zeros(len(lens), np.int64)
+    offs[1:] = np.cumsum(lens[:-1] + rng.integers(0, 5, len(lens) - 1))
+    out["random_0_2k"] = (offs, lens, 2048)
+    lens = np.concatenate([rng.integers(0, 300, 5000), [1 << 20, 3 << 20, 4096, 2049], rng.integers(0, 2049, 5000)])
+    offs = np.zeros(len(lens), np.int64)
+    offs[1:] = np.cumsum(lens[:-1] + 1)
+    out["hint_too_small"] = (offs, lens, 2048)  # the bound is wrong: still exact
+    lens = np.full(1 << 16, 64)
+    out["fixed_64B"] = (np.arange(1 << 16, dtype=np.int64) * 64, lens, 64)
+    return out
+
+
+PACKED_CASES = _packed_cases()
+
+
+@pytest.mark.parametrize("case", list(PACKED_CASES))
+def test_packed_kernel_small_records(dev, oracle_c, case):
+    """batches whose records are known to be <= 2 KiB take the packed kernel
+    (zdb_crc32_batch_device_sized, and the host-buffer entry, which measures
+    the bound itself): bit-exact against the oracle on every crafted case,
+    over both tail-pool counter parities"""
+    offs, lens, bound = PACKED_CASES[case]
+    offs = np.asarray(offs, np.int64)
+    lens = np.asarray(lens, np.int64)
+    total = int((offs + lens).max())
+    arena = oracle.splitmix_bytes(total, 77)
+    a = torch.zeros(total + 64, dtype=torch.uint8, device="cuda")
+    a[:total] = torch.from_numpy(arena).cuda()
+    o = torch.from_numpy(offs).cuda()
+    l = torch.from_numpy(lens.astype(np.int32)).cuda()
+    out = torch.full((len(lens),), -1, dtype=torch.int32, device="cuda")
+    want = oracle_c.batch(arena, offs, lens)
+    for _ in range(2):
+        dev.batch_device(a, o, l, out, max_length=bound)
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(out.cpu().numpy().view(np.uint32), want)
+    if lens.max() <= 2048:  # the host entry takes the packed kernel from the lengths themselves
+        np.testing.assert_array_equal(dev.batch_host(arena, offs.astype(np.uint64), lens.astype(np.uint32)), want)
+
+
 @pytest.mark.parametrize("case", ["one_256KiB", "eight_256KiB", "mixed_small", "at_buffer_end"])
 def test_host_batch_zero_copy(dev, oracle_c, case):
     """zdb_crc32_batch over an arena in zdb_crc32_host_alloc memory: the
