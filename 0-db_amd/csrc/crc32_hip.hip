@@ -283,6 +283,14 @@ struct SegCtx {
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef const __attribute__((address_space(1))) u32x4 global_u32x4;
 
+// a dword from global memory through a global (not flat) load: a flat load
+// counts against lgkmcnt as well as vmcnt and may complete out of order with
+// the vector loads, so while one is pending the compiler's waits on LDS
+// lookups and payload loads both become full drains
+__device__ __forceinline__ uint32_t ld_global_u32(uint64_t a) {
+    return *reinterpret_cast<const __attribute__((address_space(1))) uint32_t *>(a);
+}
+
 // zero the bytes of a piece that lie outside the record (first/last piece
 // only) and whole pieces before the segment (lanes whose load was clamped)
 __device__ __forceinline__ uint4 fix_edges(const SegCtx &s, uint4 v, uint32_t t, uint32_t lane) {
@@ -524,7 +532,7 @@ __device__ __forceinline__ uint32_t seg_value_v3(const Seg &sg, uint32_t acc, ui
     const bool fold = sg.z >= 16u;
     uint32_t y = 0;
     if (fold && sg.pb == sg.c.np)
-        y = *reinterpret_cast<const uint32_t *>(sg.c.P0 + 16u * (uint64_t)sg.c.np) & ((1u << (8u * (sg.z - 16u))) - 1u);
+        y = ld_global_u32(sg.c.P0 + 16u * (uint64_t)sg.c.np) & ((1u << (8u * (sg.z - 16u))) - 1u);
     uint32_t x = wave_xor_scalar(NOZ >= 2 ? acc : lane_place(acc, lane, lds));
     if (fold)
         x = uniform_shift(x ^ y, tables + ZDBCRC_OFF_F + (sg.z - 16u) * SCH * 32);
@@ -974,16 +982,29 @@ constexpr uint32_t PK_WP = ZDBCRC_OFF_WP - ZDBCRC_OFF_F;
 constexpr uint32_t PK_LP = ZDBCRC_OFF_LP - ZDBCRC_OFF_F;
 static_assert(ZDBCRC_OFF_F % 4 == 0 && ZDBCRC_PK_LDS_DW % 4 == 0, "packed LDS image must be 16-byte granular");
 
+// Row width RW (lanes per record; 16 unless noted): NR = 64 / RW records per
+// packet, a slot is 16 RW bytes of a row's record, a superstep PPS = K RW
+// pieces (64 RW bytes).  RW = 8 / 4 read their slot and advance tables from
+// TE/WE, TQ/WQ (copied into the TP/WP places of the LDS image) and place lane
+// l with LP's column 16 - RW + l.
+template <int RW>
+struct PkRow {
+    static constexpr uint32_t NR = 64 / RW;
+    static constexpr uint32_t PPS = K * RW;
+    static_assert(RW == 4 || RW == 8 || RW == 16, "row width");
+};
+
 // one row's record in the current packet (uniform within the row)
 struct PkGeo {
     uint64_t pb; // Ep - 1024 S + 16 l16: this lane's load address in superstep 0, slot 0
     int32_t kb;  // 64 S - np: positions before it are empty
     uint32_t fl; // lo0 | h << 4 | d << 8 | (Ep & 3) << 16
+    uint32_t y;  // the row's fold dword (vector-loaded metadata only; else PkPacket::y)
 };
 // the packet (wave-uniform)
 struct PkPacket {
     uint64_t r0;  // record of row 0 (row g: r0 + g)
-    uint32_t nr;  // rows holding a record (1..4)
+    uint32_t nr;  // rows holding a record (1..NR)
     uint32_t S;   // supersteps
     int32_t kmin; // smallest kb of the rows: slots wholly before it are empty
     int32_t kmax; // largest kb: supersteps wholly after it need no edge checks
@@ -1003,20 +1024,55 @@ __device__ __forceinline__ uint64_t row_pick64(uint32_t lane, uint64_t a, uint64
 }
 
 // descriptors of a packet's four rows (records r .. r + 3, clamped to the
-// batch), through the scalar cache: they cost no vector registers and no
-// vector-memory instructions
+// batch).  VM = false: through the scalar cache (no vector registers, no
+// vector-memory instructions -- but scalar loads share lgkmcnt with the LDS
+// lookups, so the first lookup after them waits out their whole round trip).
+// VM = true: one vector load per field, lane l holding row l / 16's
+// descriptor (the 16 lanes of a row load one address), completed in order
+// with the payload loads they are issued beside.
+template <bool VM>
 struct PkMeta {
     uint64_t o[4];
     uint32_t l[4];
 };
-__device__ __forceinline__ void pk_meta(PkMeta &m, const uint64_t *__restrict__ offsets,
-                                        const uint32_t *__restrict__ lengths, uint64_t r, uint64_t n) {
+template <>
+struct PkMeta<true> {
+    uint64_t o;
+    uint32_t l;
+};
+template <bool VM, int RW = 16>
+__device__ __forceinline__ void pk_meta(PkMeta<VM> &m, const uint64_t *__restrict__ offsets,
+                                        const uint32_t *__restrict__ lengths, uint64_t r, uint64_t n,
+                                        uint32_t lane) {
+    static_assert(VM || RW == 16, "scalar descriptors: rows of 16 only");
+    if constexpr (VM) {
+        const uint64_t rg = r + lane / RW;
+        const uint64_t i = rg < n ? rg : n - 1;
+        m.o = offsets[i];
+        m.l = lengths[i];
+    } else {
 #pragma unroll
-    for (int g = 0; g < 4; g++) {
-        const uint64_t i = r + g < n ? r + g : n - 1;
-        m.o[g] = offsets[i];
-        m.l[g] = lengths[i];
+        for (int g = 0; g < 4; g++) {
+            const uint64_t i = r + g < n ? r + g : n - 1;
+            m.o[g] = offsets[i];
+            m.l[g] = lengths[i];
+        }
     }
+}
+// this lane's row's descriptor
+template <bool VM>
+__device__ __forceinline__ uint64_t pk_addr(const PkMeta<VM> &m, uint64_t ab, uint32_t lane) {
+    if constexpr (VM)
+        return ab + m.o;
+    else
+        return ab + row_pick64(lane, m.o[0], m.o[1], m.o[2], m.o[3]);
+}
+template <bool VM>
+__device__ __forceinline__ uint32_t pk_len(const PkMeta<VM> &m, uint32_t lane) {
+    if constexpr (VM)
+        return m.l;
+    else
+        return row_pick(lane, m.l[0], m.l[1], m.l[2], m.l[3]);
 }
 
 
@@ -1026,6 +1082,20 @@ __device__ __forceinline__ uint32_t max4rows(uint32_t v) {
     const uint32_t x = a > b ? a : b, y = c > d ? c : d;
     return x > y ? x : y;
 }
+// the largest of a row-uniform value over the wave's rows of RW lanes: DPP
+// row rotations fold the rows of a 16-lane DPP row, then four readlanes
+template <int RW>
+__device__ __forceinline__ uint32_t max_rows(uint32_t v) {
+    if constexpr (RW <= 4) {
+        const uint32_t t = __builtin_amdgcn_update_dpp(0u, v, 0x124, 0xF, 0xF, false); // row_ror:4
+        v = t > v ? t : v;
+    }
+    if constexpr (RW <= 8) {
+        const uint32_t t = __builtin_amdgcn_update_dpp(0u, v, 0x128, 0xF, 0xF, false); // row_ror:8
+        v = t > v ? t : v;
+    }
+    return max4rows(v);
+}
 
 // geometry of the packet whose row g holds record rg = r0 + g (A, L: its
 // descriptor; rows at or past rb are empty), and each row's fold dword
@@ -1033,9 +1103,11 @@ __device__ __forceinline__ uint32_t max4rows(uint32_t v) {
 // table image (`dummy`), so that the loads of its empty positions -- which
 // read piece 0's address, F0 = pb + 16 (kb - l16) -- stay inside mapped memory
 // even for an empty record at the very end of the arena.
+template <bool VM, int RW = 16>
 __device__ __forceinline__ void pk_geometry(uint64_t A, uint32_t L, uint64_t r0, uint64_t rb, uint32_t lane,
                                             const uint32_t *dummy, PkGeo &g, PkPacket &p) {
-    const uint64_t rg = r0 + (lane >> 4);
+    using R = PkRow<RW>;
+    const uint64_t rg = r0 + lane / RW;
     const bool valid = rg < rb;
     if (!valid)
         L = 0;
@@ -1046,29 +1118,33 @@ __device__ __forceinline__ void pk_geometry(uint64_t A, uint32_t L, uint64_t r0,
     const uint32_t Lp = L - h;
     const uint32_t np = (Lp + 15u) >> 4;
     const uint32_t lo0 = 16u * np - Lp;
-    uint32_t S = max4rows((np + 63u) >> 6);
+    uint32_t S = max_rows<RW>((np + R::PPS - 1u) / R::PPS);
     S = S ? S : 1u;
-    const int32_t kb = (int32_t)(64u * S) - (int32_t)np;
+    const int32_t kb = (int32_t)(R::PPS * S) - (int32_t)np;
     const uint32_t kbu = (uint32_t)kb; // kb in [0, 64 S]: compare as unsigned
     p.r0 = r0;
-    p.nr = rb - r0 < 4 ? (uint32_t)(rb - r0) : 4u;
+    p.nr = rb - r0 < R::NR ? (uint32_t)(rb - r0) : R::NR;
     p.S = S;
-    p.kmax = (int32_t)max4rows(kbu);
-    p.kmin = (int32_t)(~max4rows(~kbu));
+    p.kmax = (int32_t)max_rows<RW>(kbu);
+    p.kmin = (int32_t)(~max_rows<RW>(~kbu));
     const uint64_t F0 = Ep - 16ull * np;
     const uint64_t fa = A & ~15ull;
     const uint32_t d = (np && F0 < fa && (fa & 4095ull) == 0) ? (uint32_t)(fa - F0) : 0u;
     p.anyh = __ballot(h != 0) != 0;
     p.anyd = __ballot(d != 0) != 0;
     const uint64_t ya = h ? (Ep & ~3ull) : reinterpret_cast<uint64_t>(dummy);
+    if constexpr (VM) {
+        g.y = ld_global_u32(ya); // a vector load, in order with the payload's
+    } else {
 #pragma unroll
-    for (int r = 0; r < 4; r++) {
-        const uint64_t a = ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(ya >> 32), 16 * r) << 32) |
-                           (uint32_t)__builtin_amdgcn_readlane((uint32_t)ya, 16 * r);
-        p.y[r] = *reinterpret_cast<const uint32_t *>(a);
+        for (int r = 0; r < 4; r++) {
+            const uint64_t a = ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(ya >> 32), 16 * r) << 32) |
+                               (uint32_t)__builtin_amdgcn_readlane((uint32_t)ya, 16 * r);
+            p.y[r] = ld_global_u32(a);
+        }
     }
     const uint64_t Eg = np ? Ep : reinterpret_cast<uint64_t>(dummy); // then F0 = the table image
-    g.pb = Eg - 1024ull * S + 16ull * (lane & 15u);
+    g.pb = Eg - 16ull * R::PPS * S + 16ull * (lane % RW);
     g.kb = kb;
     g.fl = lo0 | (h << 4) | (d << 8) | (((uint32_t)Ep & 3u) << 16);
 }
@@ -1111,19 +1187,20 @@ __device__ __forceinline__ uint4 pk_ld(uint64_t a) {
 // conditional: a lane that skipped one would keep its register's previous
 // value alive.  (CPU model of every address: tests/kernel_model.py
 // packed_row_crc, test_packed_loads_stay_in_bounds.)
-template <bool EDGE, bool NTL>
+template <bool EDGE, bool NTL, int RW = 16>
 __device__ __forceinline__ void pk_load(uint64_t pb, int32_t kb, uint32_t fl, uint32_t s, uint32_t lane,
                                         uint4 (&buf)[K]) {
-    const uint64_t base = pb + 1024ull * s;
+    using R = PkRow<RW>;
+    const uint64_t base = pb + 16ull * R::PPS * s;
     // piece 0's load address: F0 = Ep - 16 np, moved up to A's aligned block
     // when it would start in the page below (d); the table image for a row
     // without pieces
-    const uint64_t F0 = pb + (int64_t)16 * ((int64_t)kb - (int64_t)(lane & 15u)) + ((fl >> 8) & 15u);
+    const uint64_t F0 = pb + (int64_t)16 * ((int64_t)kb - (int64_t)(lane % RW)) + ((fl >> 8) & 15u);
 #pragma unroll
     for (int i = 0; i < K; i++) {
-        uint64_t a = base + 256u * i;
+        uint64_t a = base + 16u * RW * i;
         if (EDGE) {
-            const int32_t k = (int32_t)(64u * s + 16u * i + (lane & 15u)) - kb;
+            const int32_t k = (int32_t)(R::PPS * s + RW * i + (lane % RW)) - kb;
             a = k <= 0 ? F0 : a; // k == 0: F0 is piece 0 itself (or its safe block)
         }
         buf[i] = pk_ld<NTL>(a);
@@ -1131,7 +1208,7 @@ __device__ __forceinline__ void pk_load(uint64_t pb, int32_t kb, uint32_t fl, ui
 }
 
 // superstep s of the packet folded into the lane register
-template <bool EDGE, bool UNSAFE>
+template <bool EDGE, bool UNSAFE, int RW = 16>
 __device__ __forceinline__ uint32_t pk_superstep(const PkGeo &g, const PkPacket &p, uint32_t acc, const uint4 (&cur)[K],
                                                  uint32_t s, uint32_t lane, const uint32_t *lds) {
     if (s)
@@ -1139,8 +1216,8 @@ __device__ __forceinline__ uint32_t pk_superstep(const PkGeo &g, const PkPacket 
 #define ZDBCRC_PK_SLOT(I)                                                                           \
     if (!EDGE) {                                                                                    \
         acc ^= piece_contrib<I, 0, PK_TP>(cur[I], lds);                                             \
-    } else if ((int32_t)(64u * s + 16u * (I) + 15u) >= p.kmin) { /* not empty in every row */     \
-        const int32_t k = (int32_t)(64u * s + 16u * (I) + (lane & 15u)) - g.kb;                     \
+    } else if ((int32_t)(PkRow<RW>::PPS * s + RW * (I) + RW - 1) >= p.kmin) { /* not empty in every row */ \
+        const int32_t k = (int32_t)(PkRow<RW>::PPS * s + RW * (I) + (lane % RW)) - g.kb;           \
         uint4 v = cur[I];                                                                           \
         if (k < 0)                                                                                  \
             v = make_uint4(0, 0, 0, 0);                                                             \
@@ -1160,19 +1237,28 @@ __device__ __forceinline__ uint32_t pk_superstep(const PkGeo &g, const PkPacket 
 
 // the packet's crcs: lane placement in the row, DPP reduction over the row,
 // fold of the h bytes after the grid (every lane of a row ends with its crc)
+template <bool VM, int RW = 16>
 __device__ __forceinline__ uint32_t pk_finish(const PkGeo &g, const PkPacket &p, uint32_t acc, uint32_t lane,
                                               const uint32_t *lds) {
+    // LP column 16 - RW + (lane mod RW) holds the shift by 16 (RW - 1 - lane mod RW)
+    // (rows of 16: column lane & 31, one bank per lane; narrower rows share
+    // columns -- a 4-way conflict for rows of 4, once per packet)
+    const uint32_t col = RW == 16 ? (lane & 31u) : (16u - RW) + (lane % RW) + (lane & 16u);
     uint32_t x = 0;
 #pragma unroll
     for (int c = 0; c < SCH; c++)
-        x ^= lds[PK_LP + (c * 32 + ((acc >> (5 * c)) & 31u)) * 32 + (lane & 31u)];
+        x ^= lds[PK_LP + (c * 32 + ((acc >> (5 * c)) & 31u)) * 32 + col];
     x ^= __builtin_amdgcn_update_dpp(0u, x, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
     x ^= __builtin_amdgcn_update_dpp(0u, x, 0x4E, 0xF, 0xF, false);  // quad_perm [2,3,0,1]
-    x ^= __builtin_amdgcn_update_dpp(0u, x, 0x124, 0xF, 0xF, false); // row_ror:4
-    x ^= __builtin_amdgcn_update_dpp(0u, x, 0x128, 0xF, 0xF, false); // row_ror:8
+    if constexpr (RW == 8)
+        x ^= __builtin_amdgcn_update_dpp(0u, x, 0x141, 0xF, 0xF, false); // row_half_mirror
+    if constexpr (RW == 16) {
+        x ^= __builtin_amdgcn_update_dpp(0u, x, 0x124, 0xF, 0xF, false); // row_ror:4
+        x ^= __builtin_amdgcn_update_dpp(0u, x, 0x128, 0xF, 0xF, false); // row_ror:8
+    }
     if (p.anyh) { // F[0] is the identity: rows without fold bytes pass through
         const uint32_t h = (g.fl >> 4) & 3u;
-        const uint32_t y = row_pick(lane, p.y[0], p.y[1], p.y[2], p.y[3]);
+        const uint32_t y = VM ? g.y : row_pick(lane, p.y[0], p.y[1], p.y[2], p.y[3]);
         x ^= (y >> (8u * ((g.fl >> 16) & 3u))) & ((1u << (8u * h)) - 1u);
         uint32_t r = 0;
 #pragma unroll
@@ -1220,13 +1306,15 @@ __device__ __forceinline__ uint64_t pk_first_record(const UnitPrefix &us, uint64
 // have landed (one superstep of loads in flight per wave); 0 = two
 
 template <int WGT, int WPE, int DYN = 4, int CPW = 4, uint32_t DYN_POOLS = 32, bool SP = true, int WAITP = 0,
-          bool NTL = true>
+          bool NTL = true, bool VM = false, int RW = 16>
 __global__ __launch_bounds__(WGT, WPE) void crc_packed_kernel(
     const uint8_t *__restrict__ arena, const uint64_t *__restrict__ offsets,
     const uint32_t *__restrict__ lengths, const PlanArgs plan, uint64_t n,
     uint32_t *__restrict__ out, const uint32_t *__restrict__ tables, uint32_t max_waves,
     uint32_t *__restrict__ scratch, uint32_t epoch) {
     constexpr uint32_t NW = WGT / 64;
+    using R = PkRow<RW>;
+    constexpr uint32_t NR = R::NR;
     if (plan.dn) {
         const uint64_t dn = *plan.dn;
         n = dn < n ? dn : n;
@@ -1279,10 +1367,22 @@ __global__ __launch_bounds__(WGT, WPE) void crc_packed_kernel(
         }
     }
     {
-        const uint4 *src = reinterpret_cast<const uint4 *>(tables + ZDBCRC_OFF_F);
+        // the LDS image [F | TP | WP | LP]; narrower rows take their slot and
+        // advance tables from TE/WE or TQ/WQ
+        constexpr uint32_t TSRC = RW == 16 ? ZDBCRC_OFF_TP : RW == 8 ? ZDBCRC_OFF_TE : ZDBCRC_OFF_TQ;
+        constexpr uint32_t WSRC = RW == 16 ? ZDBCRC_OFF_WP : RW == 8 ? ZDBCRC_OFF_WE : ZDBCRC_OFF_WQ;
+        static_assert(TSRC % 4 == 0 && WSRC % 4 == 0 && PK_TP % 4 == 0 && PK_WP % 4 == 0 && PK_LP % 4 == 0,
+                      "16-byte granular table ranges");
+        const uint4 *src = reinterpret_cast<const uint4 *>(tables);
         uint4 *dst = reinterpret_cast<uint4 *>(lds);
-        for (int i = threadIdx.x; i < ZDBCRC_PK_LDS_DW / 4; i += WGT)
-            dst[i] = src[i];
+        for (uint32_t i = threadIdx.x; i < ZDBCRC_PK_LDS_DW / 4; i += WGT) {
+            const uint32_t d = 4 * i;
+            const uint32_t sdw = d < PK_TP ? ZDBCRC_OFF_F + d
+                                 : d < PK_WP ? TSRC + (d - PK_TP)
+                                 : d < PK_LP ? WSRC + (d - PK_WP)
+                                             : ZDBCRC_OFF_F + d;
+            dst[i] = src[sdw / 4];
+        }
     }
     if (blockIdx.x == 0 && threadIdx.x < DYN_MAX_POOLS) // the next launch's counters (every variant)
         scratch[SCRATCH_DYN_CTR + (((epoch + 1u) & 1u) * DYN_MAX_POOLS + threadIdx.x) * 32u] = 0u;
@@ -1329,29 +1429,28 @@ __global__ __launch_bounds__(WGT, WPE) void crc_packed_kernel(
             }
         }
         // descriptors of the range's first packet, then its geometry
-        PkMeta m;
-        pk_meta(m, offsets, lengths, r0, n);
+        PkMeta<VM> m;
+        pk_meta<VM, RW>(m, offsets, lengths, r0, n, lane);
         const uint64_t ab = reinterpret_cast<uint64_t>(arena);
         PkGeo gc;
         PkPacket pc;
-        pk_geometry(ab + row_pick64(lane, m.o[0], m.o[1], m.o[2], m.o[3]), row_pick(lane, m.l[0], m.l[1], m.l[2], m.l[3]),
-                    r0, rb, lane, dummy, gc, pc);
+        pk_geometry<VM, RW>(pk_addr<VM>(m, ab, lane), pk_len<VM>(m, lane), r0, rb, lane, dummy, gc, pc);
         uint4 cur[K], nxt[K];
         // the loads of superstep s of packet (g, p); with its first superstep,
         // the descriptors of the packet after it (scalar)
         auto issue = [&](const PkGeo &g, PkPacket &p, uint32_t s, uint4(&buf)[K]) {
             if (s == 0)
-                pk_meta(m, offsets, lengths, p.r0 + 4, n);
-            if ((int32_t)(64u * s) > p.kmax)
-                pk_load<false, NTL>(g.pb, g.kb, g.fl, s, lane, buf);
+                pk_meta<VM, RW>(m, offsets, lengths, p.r0 + NR, n, lane);
+            if ((int32_t)(R::PPS * s) > p.kmax)
+                pk_load<false, NTL, RW>(g.pb, g.kb, g.fl, s, lane, buf);
             else
-                pk_load<true, NTL>(g.pb, g.kb, g.fl, s, lane, buf);
+                pk_load<true, NTL, RW>(g.pb, g.kb, g.fl, s, lane, buf);
         };
         issue(gc, pc, 0, cur);
         uint32_t css = 0, acc = 0;
         for (;;) {
             const bool newp = css + 1 == pc.S;
-            const bool last = newp && pc.r0 + 4 >= rb; // the range ends with this packet
+            const bool last = newp && pc.r0 + NR >= rb; // the range ends with this packet
             PkGeo gn;
             PkPacket pn;
             const uint32_t nss = newp ? 0u : css + 1;
@@ -1359,28 +1458,28 @@ __global__ __launch_bounds__(WGT, WPE) void crc_packed_kernel(
                 if (WAITP)
                     __builtin_amdgcn_s_waitcnt(0x0F70);
                 if (newp) {
-                    pk_geometry(ab + row_pick64(lane, m.o[0], m.o[1], m.o[2], m.o[3]),
-                                row_pick(lane, m.l[0], m.l[1], m.l[2], m.l[3]), pc.r0 + 4, rb, lane, dummy, gn, pn);
+                    pk_geometry<VM, RW>(pk_addr<VM>(m, ab, lane), pk_len<VM>(m, lane), pc.r0 + NR, rb, lane, dummy,
+                                        gn, pn);
                     issue(gn, pn, 0, nxt);
                 } else {
                     issue(gc, pc, nss, nxt);
                 }
             }
-            if ((int32_t)(64u * css) > pc.kmax)
-                acc = pk_superstep<false, false>(gc, pc, acc, cur, css, lane, lds);
+            if ((int32_t)(R::PPS * css) > pc.kmax)
+                acc = pk_superstep<false, false, RW>(gc, pc, acc, cur, css, lane, lds);
             else if (pc.anyd)
-                acc = pk_superstep<true, true>(gc, pc, acc, cur, css, lane, lds);
+                acc = pk_superstep<true, true, RW>(gc, pc, acc, cur, css, lane, lds);
             else
-                acc = pk_superstep<true, false>(gc, pc, acc, cur, css, lane, lds);
+                acc = pk_superstep<true, false, RW>(gc, pc, acc, cur, css, lane, lds);
             uint32_t *dst = dwave;
             uint32_t x = 0;
             if (newp) {
-                x = pk_finish(gc, pc, acc, lane, lds);
+                x = pk_finish<VM, RW>(gc, pc, acc, lane, lds);
                 acc = 0;
-                if ((lane >> 4) < pc.nr)
-                    dst = out + pc.r0 + (lane >> 4);
+                if (lane / RW < pc.nr)
+                    dst = out + pc.r0 + lane / RW;
             }
-            if ((lane & 15u) == 0)
+            if (lane % RW == 0)
                 *dst = x;
             if (last)
                 break;
@@ -1468,6 +1567,17 @@ const KernelVariant kVariants[] = {
     {"pk_wg640_dyn4c4p32_sp", crc_packed_kernel<640, 5, 4, 4, 32, true, 0>, 640, WG_PER_CU, UO_PK},
     {"pk_wg640_dyn4c4p32_sp_wait", crc_packed_kernel<640, 5, 4, 4, 32, true, 1>, 640, WG_PER_CU, UO_PK},
     {"pk_wg512_dyn4c4p32_sp", crc_packed_kernel<512, 4, 4, 4, 32, true, 0>, 512, WG_PER_CU, UO_PK},
+    // round 3 (resumed): descriptors and fold dwords as vector loads (no scalar-load waits per packet)
+    {"pk_wg512_dyn4c4p32_sp_vm", crc_packed_kernel<512, 4, 4, 4, 32, true, 0, true, true>, 512, WG_PER_CU, UO_PK},
+    {"pk_wg768_dyn4c4p32_sp_vm", crc_packed_kernel<768, 6, 4, 4, 32, true, 0, true, true>, 768, WG_PER_CU, UO_PK},
+    {"pk_wg512_dyn4c4p32_sp_wait_vm", crc_packed_kernel<512, 4, 4, 4, 32, true, 1, true, true>, 512, WG_PER_CU, UO_PK},
+    {"pk_wg640_dyn4c4p32_sp_wait_vm", crc_packed_kernel<640, 5, 4, 4, 32, true, 1, true, true>, 640, WG_PER_CU, UO_PK},
+    {"pk_wg768_dyn4c4p32_sp_wait_vm", crc_packed_kernel<768, 6, 4, 4, 32, true, 1, true, true>, 768, WG_PER_CU, UO_PK},
+    // rows of 8 and 4 lanes (8 / 16 records per wave)
+    {"pk8_wg512_dyn4c4p32_sp_wait_vm", crc_packed_kernel<512, 4, 4, 4, 32, true, 1, true, true, 8>, 512, WG_PER_CU, UO_PK},
+    {"pk4_wg512_dyn4c4p32_sp_wait_vm", crc_packed_kernel<512, 4, 4, 4, 32, true, 1, true, true, 4>, 512, WG_PER_CU, UO_PK},
+    {"pk8_wg512_dyn4c4p32_sp_vm", crc_packed_kernel<512, 4, 4, 4, 32, true, 0, true, true, 8>, 512, WG_PER_CU, UO_PK},
+    {"pk4_wg512_dyn4c4p32_sp_vm", crc_packed_kernel<512, 4, 4, 4, 32, true, 0, true, true, 4>, 512, WG_PER_CU, UO_PK},
 
 };
 constexpr int kNumVariants = (int)(sizeof(kVariants) / sizeof(kVariants[0]));
@@ -1509,9 +1619,12 @@ const KernelVariant kSmall = {"v3_wg768_nt_dyn4c4p32_sp_pp_wait_bmg_xp",
                                                   false, true, true>,
                               768};
 // batches of records <= 2 KiB: the packed kernel (512 threads: the 768-thread
-// build spills, profiles/r3/ab_packed_kernel.jsonl)
-const KernelVariant kTiny = {"pk_wg512_dyn4c4p32_sp", crc_packed_kernel<512, 4, 4, 4, 32, true, 0>, 512, WG_PER_CU,
-                             UO_PK};
+// build spills, profiles/r3/ab_packed_kernel.jsonl) with vector-loaded
+// descriptors and fold dwords and one superstep of loads in flight
+// (fixed 2 KiB -16 %, Zipf <= 2 KiB -13 %, 256 B records -23 % against the
+// scalar-loaded first version, profiles/r3/ab_packed_vm*.jsonl)
+const KernelVariant kTiny = {"pk_wg512_dyn4c4p32_sp_wait_vm", crc_packed_kernel<512, 4, 4, 4, 32, true, 1, true, true>,
+                             512, WG_PER_CU, UO_PK};
 // the kernel for a batch whose records are at most max_len bytes (0: unknown)
 const KernelVariant &variant(uint64_t max_len = 0) {
     if (max_len == 0 || max_len > SMALL_RECORD_MAX)
@@ -1717,6 +1830,40 @@ __global__ __launch_bounds__(256) void stream_read_kernel(const uint4 *__restric
 // contiguous-slice variant of the probe: wave w reads its own slice, 1 KiB
 // per load instruction, U loads per lane per iteration -- the access shape of
 // crc_batch_kernel without any checksum work
+// read probe of the packed kernels' access shape: the arena as 4 KiB
+// records, a wave walking packets of 64 / RW records, row g (RW lanes) on
+// record g of the packet, U loads of RW x 16 B per row in flight (each load
+// instruction touches 64 / RW separate RW x 16-byte segments), nontemporal
+template <int RW, int U>
+__global__ __launch_bounds__(1024) void stream_rows_kernel(const uint4 *__restrict__ src, uint64_t words,
+                                                           uint32_t *__restrict__ sink) {
+    constexpr uint64_t REC_W = 256, NR = 64 / RW;
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t nw = (uint64_t)gridDim.x * (blockDim.x / 64);
+    const uint64_t w = (uint64_t)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
+    const uint64_t npk = words / REC_W / NR;
+    const uint64_t lo = npk * w / nw, hi = npk * (w + 1) / nw;
+    uint4 a = make_uint4(0, 0, 0, 0);
+    for (uint64_t pk = lo; pk < hi; pk++) {
+        const uint64_t base = pk * NR * REC_W + (lane / RW) * REC_W + (lane % RW);
+        for (uint32_t j = 0; j < REC_W / RW; j += U) {
+            uint4 x[U];
+#pragma unroll
+            for (int u = 0; u < U; u++) {
+                const u32x4 t = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(src + base + RW * (j + u)));
+                x[u] = make_uint4(t.x, t.y, t.z, t.w);
+            }
+#pragma unroll
+            for (int u = 0; u < U; u++) {
+                a.x ^= x[u].x; a.y ^= x[u].y; a.z ^= x[u].z; a.w ^= x[u].w;
+            }
+        }
+    }
+    uint32_t v = wave_xor(a.x ^ a.y ^ a.z ^ a.w);
+    if (lane == 0)
+        atomicXor(sink + (w & 0xFFFF), v);
+}
+
 template <int U, bool NTL = false>
 __global__ __launch_bounds__(1024) void stream_slice_kernel(const uint4 *__restrict__ src, uint64_t words,
                                                             uint32_t *__restrict__ sink) {
@@ -2128,6 +2275,16 @@ float zdbcrc_debug_stream_read(const void *d_buf, size_t bytes, uint32_t *d_sink
         hipLaunchKernelGGL((stream_slice_kernel<4, true>), dim3(512), dim3(768), 0, st, src, words, d_sink);
     else if (blocks == -108)
         hipLaunchKernelGGL((stream_slice_kernel<8, true>), dim3(512), dim3(1024), 0, st, src, words, d_sink);
+    else if (blocks == -304) // packed access shapes (stream_rows_kernel): rows of 4 / 8 / 16 / 64 lanes
+        hipLaunchKernelGGL((stream_rows_kernel<4, 4>), dim3(512), dim3(1024), 0, st, src, words, d_sink);
+    else if (blocks == -308)
+        hipLaunchKernelGGL((stream_rows_kernel<8, 4>), dim3(512), dim3(1024), 0, st, src, words, d_sink);
+    else if (blocks == -316)
+        hipLaunchKernelGGL((stream_rows_kernel<16, 4>), dim3(512), dim3(1024), 0, st, src, words, d_sink);
+    else if (blocks == -364)
+        hipLaunchKernelGGL((stream_rows_kernel<64, 4>), dim3(512), dim3(1024), 0, st, src, words, d_sink);
+    else if (blocks == -344) // rows of 4 lanes, 8 loads in flight
+        hipLaunchKernelGGL((stream_rows_kernel<4, 8>), dim3(512), dim3(1024), 0, st, src, words, d_sink);
     else
         hipLaunchKernelGGL(stream_slice_kernel<16>, dim3(512), dim3(1024), 0, st, src, words, d_sink);
     hipEventRecord(b, st);

@@ -214,6 +214,26 @@ void zdbcrc_build_tables(uint32_t *img) {
             b[t] = multmodp(mwp, reg_slice(1u << t, c));
         fill_linear(img + ZDBCRC_OFF_WP + c * 32, 1, b);
     }
+    /* narrower rows: 8 lanes (128 B per slot), 4 lanes (64 B per slot) */
+    for (int nr = 0; nr < 2; nr++) {
+        const uint64_t slot = nr ? 64 : 128;
+        uint32_t *const tt = img + (nr ? ZDBCRC_OFF_TQ : ZDBCRC_OFF_TE);
+        uint32_t *const tw = img + (nr ? ZDBCRC_OFF_WQ : ZDBCRC_OFF_WE);
+        for (int i = 0; i < ZDBCRC_K; i++) {
+            const uint32_t m = xpow(8 * slot * (uint64_t)(ZDBCRC_K - 1 - i), 0);
+            for (int c = 0; c < ZDBCRC_PCH; c++) {
+                for (int t = 0; t < 5; t++)
+                    b[t] = multmodp(m, piece_window_crc(1u << t, c));
+                fill_linear(tt + (i * ZDBCRC_PCH + c) * 32, 1, b);
+            }
+        }
+        const uint32_t mw2 = xpow(8 * slot * (uint64_t)ZDBCRC_K, 0);
+        for (int c = 0; c < ZDBCRC_SCH; c++) {
+            for (int t = 0; t < 5; t++)
+                b[t] = multmodp(mw2, reg_slice(1u << t, c));
+            fill_linear(tw + c * 32, 1, b);
+        }
+    }
     for (int l = 0; l < 32; l++) {
         const uint32_t m = xpow(8 * 16 * (uint64_t)(15 - (l & 15)), 0);
         for (int c = 0; c < ZDBCRC_SCH; c++) {

@@ -57,8 +57,14 @@ uint32_t zdbcrc_update_bytes(uint32_t crc, const uint8_t *p, size_t n);
 #define ZDBCRC_OFF_TP   (ZDBCRC_OFF_F + 4 * ZDBCRC_SCH * 32)                /* [K][PCH][32]      */
 #define ZDBCRC_OFF_WP   (ZDBCRC_OFF_TP + ZDBCRC_K * ZDBCRC_PCH * 32)        /* [SCH][32]         */
 #define ZDBCRC_OFF_LP   (ZDBCRC_OFF_WP + ZDBCRC_SCH * 32)                   /* [SCH][32][32]     */
-#define ZDBCRC_TABLE_DW (ZDBCRC_OFF_LP + ZDBCRC_SCH * 32 * 32)
-#define ZDBCRC_PK_LDS_DW (ZDBCRC_TABLE_DW - ZDBCRC_OFF_F)
+#define ZDBCRC_PK_LDS_DW (ZDBCRC_OFF_LP + ZDBCRC_SCH * 32 * 32 - ZDBCRC_OFF_F)
+/* the same kernel with narrower rows (8 / 4 lanes: 8 / 16 records per wave):
+ * its slot and advance tables; F and LP are shared */
+#define ZDBCRC_OFF_TE   (ZDBCRC_OFF_LP + ZDBCRC_SCH * 32 * 32)              /* [K][PCH][32] rows of 8 */
+#define ZDBCRC_OFF_WE   (ZDBCRC_OFF_TE + ZDBCRC_K * ZDBCRC_PCH * 32)        /* [SCH][32]            */
+#define ZDBCRC_OFF_TQ   (ZDBCRC_OFF_WE + ZDBCRC_SCH * 32)                   /* [K][PCH][32] rows of 4 */
+#define ZDBCRC_OFF_WQ   (ZDBCRC_OFF_TQ + ZDBCRC_K * ZDBCRC_PCH * 32)        /* [SCH][32]            */
+#define ZDBCRC_TABLE_DW (ZDBCRC_OFF_WQ + ZDBCRC_SCH * 32)
 
 /*
  * Piece windows.  A 16-byte piece (dwords w0..w3, little endian) is covered
@@ -97,6 +103,10 @@ int zdbcrc_window_bit(int j, int t);
  * WP[c][v]   : shift(v << 5c, 1024)           (row register across a superstep)
  * LP[c][v][l]: shift(v << 5c, 16*(15-(l&15))), l = lane & 31 (lane l's
  *              placement in its row; 32 columns so that bank = lane & 31)
+ * Rows of RW = 8 / 4 lanes (16 RW bytes per slot, 64 RW per superstep):
+ * TE, TQ[i][j][v]: as T, shifted by 16 RW (K-1-i) bytes
+ * WE, WQ[c][v]   : shift(v << 5c, 64 RW)
+ * (placement by 16 (RW-1-l) bytes reads LP's column 16 - RW + l)
  */
 void zdbcrc_build_tables(uint32_t *image /* ZDBCRC_TABLE_DW dwords */);
 

@@ -22,7 +22,12 @@ OFF_F = OFF_R + RDIG * 256 * SCH * 32
 OFF_TP = OFF_F + 4 * SCH * 32  # packed kernel: [K][PCH][32] slot tables (256 B per slot)
 OFF_WP = OFF_TP + K * PCH * 32   # [SCH][32] advance over one packed superstep (1 KiB)
 OFF_LP = OFF_WP + SCH * 32       # [SCH][32][32] placement of lane l & 31 in its row of 16
-TABLE_DW = OFF_LP + SCH * 32 * 32
+OFF_TE = OFF_LP + SCH * 32 * 32  # rows of 8 lanes: slot tables (128 B per slot)
+OFF_WE = OFF_TE + K * PCH * 32   # ... advance over 512 B
+OFF_TQ = OFF_WE + SCH * 32       # rows of 4 lanes: slot tables (64 B per slot)
+OFF_WQ = OFF_TQ + K * PCH * 32   # ... advance over 256 B
+TABLE_DW = OFF_WQ + SCH * 32
+PK_TABLES = {16: (OFF_TP, OFF_WP), 8: (OFF_TE, OFF_WE), 4: (OFF_TQ, OFF_WQ)}
 UNIT_OVH = 384
 DWG_MIN_BYTES = 64 * 1024  # record-relative grids this long load from the dword below the record
 MIN_UNITS_PER_WAVE = 256
@@ -215,10 +220,7 @@ def batch(arena: np.ndarray, offsets, lengths, tab: np.ndarray, max_waves: int =
 
 # ------------------------------------------------------------ packed kernel --
 
-ROW = np.arange(16, dtype=np.int64)
-
-
-def packed_geometry(A: int, L: int) -> dict:
+def packed_geometry(A: int, L: int, rw: int = 16) -> dict:
     """One record's grid in crc_packed_kernel: pieces end at the dword Ep at or
     below the record's end E; the h = min(E & 3, L) bytes after it are folded
     in at the end, crc(X || y) = shift(crc(X) ^ y, h); piece 0 starts lo0
@@ -227,18 +229,22 @@ def packed_geometry(A: int, L: int) -> dict:
     h = min(E & 3, L)
     Ep = E - h
     np_ = (L - h + 15) >> 4
-    return {"E": E, "h": h, "Ep": Ep, "np": np_, "lo0": 16 * np_ - (L - h), "S": (np_ + 63) >> 6}
+    pps = K * rw  # pieces of a row per superstep
+    return {"E": E, "h": h, "Ep": Ep, "np": np_, "lo0": 16 * np_ - (L - h), "S": (np_ + pps - 1) // pps}
 
 
 def packed_row_crc(mem: np.ndarray, mem_base: int, A: int, L: int, S: int, row: int, tab: np.ndarray,
-                   force_shifted_first: bool = False) -> int:
-    """The crc one row of 16 lanes computes for record (A, L) in a packet of S
-    supersteps (S >= the record's own): position q = 64 s + 16 i + l16 holds
-    piece k = q - (64 S - np) (k < 0: empty), loaded from Ep - 16 (64 S - q).
+                   force_shifted_first: bool = False, rw: int = 16) -> int:
+    """The crc one row of rw lanes computes for record (A, L) in a packet of S
+    supersteps (S >= the record's own): with P = 4 rw pieces per superstep,
+    position q = P s + rw i + l holds piece k = q - (P S - np) (k < 0: empty),
+    loaded from Ep - 16 (P S - q).
     force_shifted_first: load every first piece the way the kernel loads one
     that starts in an unmapped page (the aligned block holding A, moved up)."""
-    g = packed_geometry(A, L)
-    kbase = 64 * S - g["np"]
+    g = packed_geometry(A, L, rw)
+    P = K * rw
+    off_t, off_w = PK_TABLES[rw]
+    kbase = P * S - g["np"]
     # what the kernel may read: A's 4 KiB page from A's 16-byte block on, up to
     # the 16-byte boundary after the record's last byte
     lo_ok, hi_ok = ((A & ~15) & ~4095), (g["E"] + 15) & ~15
@@ -250,21 +256,21 @@ def packed_row_crc(mem: np.ndarray, mem_base: int, A: int, L: int, S: int, row: 
 
     if g["h"]:
         check(g["Ep"] & ~3, 4)
-    acc = np.zeros(16, dtype=np.uint32)
+    acc = np.zeros(rw, dtype=np.uint32)
     for s in range(S):
         if s:
             sl = _slices32(acc)
-            acc = np.bitwise_xor.reduce(tab[OFF_WP + np.arange(SCH) * 32 + sl], axis=1).astype(np.uint32)
+            acc = np.bitwise_xor.reduce(tab[off_w + np.arange(SCH) * 32 + sl], axis=1).astype(np.uint32)
         for i in range(K):
-            words = np.zeros((16, 4), dtype=np.uint32)
-            for l16 in range(16):
-                q = 64 * s + 16 * i + l16
+            words = np.zeros((rw, 4), dtype=np.uint32)
+            for l16 in range(rw):
+                q = P * s + rw * i + l16
                 k = q - kbase
                 if g["np"]:  # the kernel's load: positions k <= 0 read piece 0 (at F0 + d)
-                    check(F0 + d if k <= 0 else g["Ep"] - 16 * (64 * S - q), 16)
+                    check(F0 + d if k <= 0 else g["Ep"] - 16 * (P * S - q), 16)
                 if k < 0:
                     continue
-                addr = g["Ep"] - 16 * (64 * S - q)
+                addr = g["Ep"] - 16 * (P * S - q)
                 if k == 0 and force_shifted_first and addr < (A & ~15):
                     blk = mem[(A & ~15) - mem_base:(A & ~15) - mem_base + 16]
                     d = (A & ~15) - addr  # the block holds piece bytes [d, 16)
@@ -276,11 +282,13 @@ def packed_row_crc(mem: np.ndarray, mem_base: int, A: int, L: int, S: int, row: 
                     b[:g["lo0"]] = 0
                 words[l16] = b.view("<u4")
             sl = _slices128(words)
-            idx = OFF_TP + (i * PCH + np.arange(PCH)) * 32 + sl
+            idx = off_t + (i * PCH + np.arange(PCH)) * 32 + sl
             acc ^= np.bitwise_xor.reduce(tab[idx], axis=1).astype(np.uint32)
     sl = _slices32(acc)
-    lane32 = (16 * row + ROW) & 31
-    idx = OFF_LP + (np.arange(SCH)[None, :] * 32 + sl) * 32 + lane32[:, None]
+    lanes = rw * row + np.arange(rw, dtype=np.int64)
+    # LP column of lane l: l & 31 for rows of 16, else 16 - rw + l mod rw (+16 in the upper half)
+    col = lanes & 31 if rw == 16 else (16 - rw) + lanes % rw + (lanes & 16)
+    idx = OFF_LP + (np.arange(SCH)[None, :] * 32 + sl) * 32 + col[:, None]
     x = int(np.bitwise_xor.reduce(np.bitwise_xor.reduce(tab[idx], axis=1)))
     if g["h"]:
         y = int.from_bytes(mem[g["Ep"] - mem_base:g["E"] - mem_base].tobytes(), "little")
@@ -289,9 +297,10 @@ def packed_row_crc(mem: np.ndarray, mem_base: int, A: int, L: int, S: int, row: 
 
 
 def packed_batch(arena: np.ndarray, offsets, lengths, tab: np.ndarray, base_addr: int = 0,
-                 force_shifted_first: bool = False) -> np.ndarray:
-    """out[r] as crc_packed_kernel computes it: records four at a time (rows
-    0..3 of a wave), every packet as many supersteps as its longest record."""
+                 force_shifted_first: bool = False, rw: int = 16) -> np.ndarray:
+    """out[r] as crc_packed_kernel<RW = rw> computes it: records 64 / rw at a
+    time (rows of a wave), every packet as many supersteps as its longest record."""
+    nr = 64 // rw
     offsets = np.asarray(offsets, dtype=np.int64)
     lengths = np.asarray(lengths, dtype=np.int64)
     n = len(offsets)
@@ -300,9 +309,9 @@ def packed_batch(arena: np.ndarray, offsets, lengths, tab: np.ndarray, base_addr
     mem = np.zeros(pad_lo + len(arena) + 32, dtype=np.uint8)
     mem[pad_lo:pad_lo + len(arena)] = arena
     mem_base = base_addr - pad_lo
-    for r0 in range(0, n, 4):
-        recs = [(base_addr + int(offsets[r]), int(lengths[r])) for r in range(r0, min(n, r0 + 4))]
-        S = max(packed_geometry(a, L)["S"] for a, L in recs)
+    for r0 in range(0, n, nr):
+        recs = [(base_addr + int(offsets[r]), int(lengths[r])) for r in range(r0, min(n, r0 + nr))]
+        S = max(max(packed_geometry(a, L, rw)["S"] for a, L in recs), 1)
         for g, (a, L) in enumerate(recs):
-            out[r0 + g] = packed_row_crc(mem, mem_base, a, L, S, g, tab, force_shifted_first)
+            out[r0 + g] = packed_row_crc(mem, mem_base, a, L, S, g, tab, force_shifted_first, rw)
     return out

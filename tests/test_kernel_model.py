@@ -139,14 +139,15 @@ def test_tail_pool_guard():
     assert len(km.ranges(10 ** 7, 16, 64 * chunk + 1, 16, dyn=6, pools=8)) == 16
 
 
+@pytest.mark.parametrize("rw", [16, 8, 4])
 @pytest.mark.parametrize("force_shifted_first", [False, True])
 @pytest.mark.parametrize("base", [0, 1, 2, 3, 13])
-def test_packed_small_records(oracle_c, tab, base, force_shifted_first):
-    """the packed small-record kernel's math (rows of 16 lanes, 256 B per
-    slot, dword-anchored grid + h-byte fold, packets as long as their longest
-    record): lengths 0..4 KiB at every alignment, including records shorter
-    than their fold and packets mixing 1..4 supersteps; and the first-piece
-    path the kernel takes when a piece would start in the page below"""
+def test_packed_small_records(oracle_c, tab, base, force_shifted_first, rw):
+    """the packed small-record kernel's math (rows of rw = 16 / 8 / 4 lanes,
+    16 rw bytes per slot, dword-anchored grid + h-byte fold, packets as long as
+    their longest record): lengths 0..4 KiB at every alignment, including
+    records shorter than their fold and packets mixing supersteps; and the
+    first-piece path the kernel takes when a piece would start in the page below"""
     rng = np.random.default_rng(300 + base)
     lens = np.concatenate([np.arange(0, 40), rng.integers(0, 4097, 120), [4096] * 8, [4095, 4097, 1024, 1023, 1025]])
     rng.shuffle(lens)
@@ -155,19 +156,21 @@ def test_packed_small_records(oracle_c, tab, base, force_shifted_first):
     offs[1:] = np.cumsum(lens[:-1] + gaps[:-1])
     offs += 1
     arena = oracle.splitmix_bytes(int(offs[-1] + lens[-1]) + 16, 300 + base)
-    got = km.packed_batch(arena, offs, lens, tab, base_addr=base, force_shifted_first=force_shifted_first)
+    got = km.packed_batch(arena, offs, lens, tab, base_addr=base, force_shifted_first=force_shifted_first, rw=rw)
     np.testing.assert_array_equal(got, oracle_c.batch(arena, offs, lens))
 
 
-def test_packed_long_record_in_packet(oracle_c, tab):
+@pytest.mark.parametrize("rw", [16, 8, 4])
+def test_packed_long_record_in_packet(oracle_c, tab, rw):
     """a record longer than 4 KiB (a wrong max_length hint) stretches its packet: still exact"""
     lens = np.array([5, 70_000, 4096, 0, 33, 9000])
     offs = np.array([0, 7, 70_011, 74_200, 74_200, 74_300])
     arena = oracle.splitmix_bytes(90_000, 9)
-    np.testing.assert_array_equal(km.packed_batch(arena, offs, lens, tab), oracle_c.batch(arena, offs, lens))
+    np.testing.assert_array_equal(km.packed_batch(arena, offs, lens, tab, rw=rw), oracle_c.batch(arena, offs, lens))
 
 
-def test_packed_loads_stay_in_bounds(oracle_c, tab):
+@pytest.mark.parametrize("rw", [16, 4])
+def test_packed_loads_stay_in_bounds(oracle_c, tab, rw):
     """every load the packed kernel issues (empty positions included) stays in
     A's 4 KiB page from A's 16-byte block on and below the 16-byte boundary
     after the record (packed_row_crc asserts it): records at the first bytes
@@ -180,5 +183,5 @@ def test_packed_loads_stay_in_bounds(oracle_c, tab):
                 lens.append(L)
     offs, lens = np.array(offs), np.array(lens)
     arena = oracle.splitmix_bytes(int(offs.max() + lens.max()) + 32, 5)
-    got = km.packed_batch(arena, offs, lens, tab, base_addr=1 << 20)
+    got = km.packed_batch(arena, offs, lens, tab, base_addr=1 << 20, rw=rw)
     np.testing.assert_array_equal(got, oracle_c.batch(arena, offs, lens))
