@@ -1461,6 +1461,18 @@ constexpr uint32_t DENSITY_SAMPLE = 64u << 10;
 constexpr uint32_t DENSITY_MAX_PER_CHUNK = 512; // records per default chunk before it is made smaller
 constexpr uint32_t DENSITY_TARGET = 128;        // records per chunk when it is
 constexpr uint32_t MIN_LG_CHUNK = 16;
+// a store whose default chunks outnumber the search workgroups the GPU holds
+// at once (6 per CU at <= 80 VGPRs) walks in chunks twice as large, when its
+// density keeps them within half their slots: the last chunks no longer wait
+// 100-170 us for a free slot (C4: 2,048 chunks, 1,536 resident; stamped
+// span 440 -> 391 us, profiles/r3/walk_width_chunk.jsonl)
+constexpr uint32_t SEARCH_WG_PER_CU = 6;
+constexpr uint32_t LARGE_LG_CHUNK = 24;
+// record slots per chunk (beyond them a chunk's records are emitted by a
+// serial re-walk): 512, 1,024 for the large chunks
+__host__ __device__ constexpr uint32_t chunk_slots(uint32_t lg, uint64_t nchunks) {
+    return nchunks > 65536 ? 64u : lg >= LARGE_LG_CHUNK ? 1024u : 512u;
+}
 
 __global__ __launch_bounds__(64) void walk_density_kernel(FileTab t, unsigned long long *__restrict__ acc) {
     __shared__ __attribute__((aligned(16))) uint32_t lds[4096 / 4 + 4];
@@ -1567,6 +1579,14 @@ int zdb_datafile_walk_device(const uint8_t *d_image, const uint64_t *d_file_off,
                 const double c = (double)DENSITY_TARGET * (double)h[1] / (double)h[0]; // bytes per target chunk
                 while (lg > MIN_LG_CHUNK && (double)(1ull << lg) > c)
                     lg--;
+            } else if (h[0] && h[1]) {
+                int cus = 0;
+                const uint64_t n8 = (max_file_len + (1ull << DEFAULT_LG_CHUNK) - 1) >> DEFAULT_LG_CHUNK;
+                if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
+                    cus > 0 && n8 * nfiles > (uint64_t)cus * SEARCH_WG_PER_CU &&
+                    (double)h[0] * (double)(1ull << LARGE_LG_CHUNK) <=
+                        0.5 * chunk_slots(LARGE_LG_CHUNK, 1) * (double)h[1])
+                    lg = LARGE_LG_CHUNK;
             }
             g_walk_lg[dev][key] = lg;
         }
@@ -1576,11 +1596,11 @@ int zdb_datafile_walk_device(const uint8_t *d_image, const uint64_t *d_file_off,
     // one search workgroup of SEARCH_T threads per chunk and up to 512 slot
     // threads per chunk in the copy: keep every grid below 2^32 threads, so
     // an oversized store fails here and not as a late launch error
-    if (nchunks >= (1ull << 32) / SEARCH_T || nchunks * (nchunks <= 65536 ? 512u : 64u) >= (1ull << 32))
+    const uint32_t kcap = chunk_slots(lg, nchunks);
+    if (nchunks >= (1ull << 32) / SEARCH_T || nchunks * kcap >= (1ull << 32))
         return ZDB_CRC32_EINVAL;
     // workspace: per chunk s_start, s_exit, true_start, chunk_base (u64),
     // s_count, s_status, chunk_mode (4 B), kcap record slots (16 B each)
-    const uint32_t kcap = nchunks <= 65536 ? 512u : 64u;
     auto al = [](size_t x) { return (x + 255) & ~size_t(255); };
     // (+ the stitch's ticket counter, zero between walks)
     const size_t need = 4 * al(nchunks * 8) + 3 * al(nchunks * 4) + al(nchunks * kcap * sizeof(RecSlot)) + 256;
@@ -1642,23 +1662,26 @@ int zdb_datafile_walk_device(const uint8_t *d_image, const uint64_t *d_file_off,
     hipLaunchKernelGGL((walk_search_chain_kernel<SEARCH_T, SEARCH_SU, SEARCH_MW, WBV, true>),                          \
                        dim3((uint32_t)nchunks), dim3(SEARCH_T), 0, st, t, s_start, s_status, s_exit, s_count, slots,   \
                        kcap, g_stamps)
-        if (search_nt() == 512 || search_nt() == 1024) { // A/B: more waves per chunk search
+        if (search_nt() == 384 || search_nt() == 512 || search_nt() == 768 || search_nt() == 1024) {
+            // A/B: more waves per chunk search
             const bool stamp = g_stamps && nchunks <= g_stamps_n;
             if (stamp)
                 g_stamps_used = nchunks;
             uint64_t *sp = stamp ? g_stamps : nullptr;
-            if (search_nt() == 512 && stamp)
-                hipLaunchKernelGGL((walk_search_chain_kernel<512, SEARCH_SU, SEARCH_MW, 2048, true>), dim3((uint32_t)nchunks),
-                                   dim3(512), 0, st, t, s_start, s_status, s_exit, s_count, slots, kcap, sp);
-            else if (search_nt() == 512)
-                hipLaunchKernelGGL((walk_search_chain_kernel<512, SEARCH_SU, SEARCH_MW, 2048, false>), dim3((uint32_t)nchunks),
-                                   dim3(512), 0, st, t, s_start, s_status, s_exit, s_count, slots, kcap, sp);
-            else if (stamp)
-                hipLaunchKernelGGL((walk_search_chain_kernel<1024, SEARCH_SU, SEARCH_MW, 2048, true>), dim3((uint32_t)nchunks),
-                                   dim3(1024), 0, st, t, s_start, s_status, s_exit, s_count, slots, kcap, sp);
-            else
-                hipLaunchKernelGGL((walk_search_chain_kernel<1024, SEARCH_SU, SEARCH_MW, 2048, false>), dim3((uint32_t)nchunks),
-                                   dim3(1024), 0, st, t, s_start, s_status, s_exit, s_count, slots, kcap, sp);
+#define ZDBCRC_NT(N)                                                                                                   \
+    if (search_nt() == N) {                                                                                            \
+        if (stamp)                                                                                                     \
+            hipLaunchKernelGGL((walk_search_chain_kernel<N, SEARCH_SU, SEARCH_MW, 2048, true>), dim3((uint32_t)nchunks), \
+                               dim3(N), 0, st, t, s_start, s_status, s_exit, s_count, slots, kcap, sp);                \
+        else                                                                                                           \
+            hipLaunchKernelGGL((walk_search_chain_kernel<N, SEARCH_SU, SEARCH_MW, 2048, false>), dim3((uint32_t)nchunks), \
+                               dim3(N), 0, st, t, s_start, s_status, s_exit, s_count, slots, kcap, sp);                \
+    }
+            ZDBCRC_NT(384)
+            ZDBCRC_NT(512)
+            ZDBCRC_NT(768)
+            ZDBCRC_NT(1024)
+#undef ZDBCRC_NT
         } else if (search_ilp() != SEARCH_ILP) {
             if (search_ilp_mw() == 5)
                 hipLaunchKernelGGL((walk_search_chain_kernel<SEARCH_T, SEARCH_SU, 5, 0, false, !SEARCH_ILP>),
