@@ -448,7 +448,7 @@ __device__ __forceinline__ void load_meta(MetaBatch &m, uint64_t rb, uint64_t n,
     }
 }
 
-template <uint32_t UO, bool BMG = false>
+template <uint32_t UO, bool BMG = false, uint64_t DWGM = DWG_MIN_BYTES>
 __device__ __forceinline__ bool next_seg_batched(uint64_t &r, uint64_t n, uint64_t ub, uint64_t ue, uint32_t lane,
                                                  MetaBatch &m, const UnitPrefix &unit_start,
                                                  const uint8_t *arena, const uint64_t *__restrict__ offsets,
@@ -483,7 +483,7 @@ __device__ __forceinline__ bool next_seg_batched(uint64_t &r, uint64_t n, uint64
             // (seg_value_v3, z = 16 + h); aligned grid: z = the trailing pad of
             // the last piece.  BMG (A/B only): byte-misaligned loads for all
             const bool rel = sg.c.np != (uint32_t)pieces_aligned(A, Aend - A);
-            const uint32_t h = rel && !BMG && Aend - A >= DWG_MIN_BYTES ? (uint32_t)(A & 3u) : 0u;
+            const uint32_t h = rel && !BMG && Aend - A >= DWGM ? (uint32_t)(A & 3u) : 0u;
             sg.c.P0 = rel ? A - h : (A & ~15ull);
             sg.z = rel ? (h ? 16u + h : 0u) : (uint32_t)(sg.c.P0 + 16u * (uint64_t)sg.c.np - Aend);
             sg.c.lo0 = rel ? (int)h : (int)(A & 15u);
@@ -609,7 +609,8 @@ __device__ __forceinline__ uint64_t block_excl_scan64(uint64_t v, uint64_t *wsum
 // are flushed with atomic XOR at each claim (at most 2 are pending then).
 template <int WGT, int WPE, bool STAMP = false, int PRIO = 0, uint32_t UO = UNIT_OVH, int NOZ = 0,
           bool NTL = false, bool NOLOAD = false, int XM = 0, int DYN = 0, int CPW = 4, uint32_t DYN_POOLS = 8,
-          bool SP = false, int PP = 0, bool SEGDUMP = false, bool BMG = false, bool XP = false>
+          bool SP = false, int PP = 0, bool SEGDUMP = false, bool BMG = false, bool XP = false,
+          uint64_t DWGM = DWG_MIN_BYTES>
 __global__ __launch_bounds__(WGT, WPE) void crc_batch_kernel_v3(
     const uint8_t *__restrict__ arena, const uint64_t *__restrict__ offsets,
     const uint32_t *__restrict__ lengths, const PlanArgs plan, uint64_t n,
@@ -699,7 +700,7 @@ __global__ __launch_bounds__(WGT, WPE) void crc_batch_kernel_v3(
     if (active) {
         rn = find_record(unit_start, n, ub, lane);
         load_meta(m, rn, n, lane, unit_start, arena, offsets, lengths);
-        active = next_seg_batched<UO, BMG>(rn, n, ub, ue, lane, m, unit_start, arena, offsets, lengths, cur);
+        active = next_seg_batched<UO, BMG, DWGM>(rn, n, ub, ue, lane, m, unit_start, arena, offsets, lengths, cur);
         if (active)
             load_superstep_v3<NTL, NOLOAD>(cur.c, 0, lane, bufc);
     }
@@ -770,7 +771,7 @@ __global__ __launch_bounds__(WGT, WPE) void crc_batch_kernel_v3(
             rn = find_record(unit_start, n, ub, lane);
             if (rn < m.rb)
                 load_meta(m, rn, n, lane, unit_start, arena, offsets, lengths);
-            if (next_seg_batched<UO, BMG>(rn, n, ub, ue, lane, m, unit_start, arena, offsets, lengths, sg))
+            if (next_seg_batched<UO, BMG, DWGM>(rn, n, ub, ue, lane, m, unit_start, arena, offsets, lengths, sg))
                 return true;
         }
     };
@@ -831,7 +832,7 @@ __global__ __launch_bounds__(WGT, WPE) void crc_batch_kernel_v3(
         if (css + 1 < cur.S) {                                                                                \
             nx = cur;                                                                                         \
             nss = css + 1;                                                                                    \
-        } else if (!next_seg_batched<UO, BMG>(rn, n, ub, ue, lane, m, unit_start, arena, offsets, lengths, nx) &&  \
+        } else if (!next_seg_batched<UO, BMG, DWGM>(rn, n, ub, ue, lane, m, unit_start, arena, offsets, lengths, nx) &&  \
                    !(DYN && dyn && claim(nx))) {                                                              \
             more = false;                                                                                     \
             nx = cur;                                                                                         \
@@ -1573,6 +1574,10 @@ const KernelVariant kVariants[] = {
     {"pk_wg512_dyn4c4p32_sp_wait_vm", crc_packed_kernel<512, 4, 4, 4, 32, true, 1, true, true>, 512, WG_PER_CU, UO_PK},
     {"pk_wg640_dyn4c4p32_sp_wait_vm", crc_packed_kernel<640, 5, 4, 4, 32, true, 1, true, true>, 640, WG_PER_CU, UO_PK},
     {"pk_wg768_dyn4c4p32_sp_wait_vm", crc_packed_kernel<768, 6, 4, 4, 32, true, 1, true, true>, 768, WG_PER_CU, UO_PK},
+    // round 3 (resumed): the dword grid for record-relative records of every size, now that its fold dword
+    // is a global (not flat) load -- small shape and default
+    {"v3_wg768_nt_dyn4c4p32_sp_pp_wait_dwg0_xp", crc_batch_kernel_v3<768, 6, false, 0, UNIT_OVH, false, true, false, 0, 4, 4, 32, true, 3, false, false, true, 0>, 768},
+    {"v3_wg768_nt_dyn4c4p32_sp_dwg0_xp", crc_batch_kernel_v3<768, 6, false, 0, UNIT_OVH, false, true, false, 0, 4, 4, 32, true, 0, false, false, true, 0>, 768},
     // rows of 8 and 4 lanes (8 / 16 records per wave)
     {"pk8_wg512_dyn4c4p32_sp_wait_vm", crc_packed_kernel<512, 4, 4, 4, 32, true, 1, true, true, 8>, 512, WG_PER_CU, UO_PK},
     {"pk4_wg512_dyn4c4p32_sp_wait_vm", crc_packed_kernel<512, 4, 4, 4, 32, true, 1, true, true, 4>, 512, WG_PER_CU, UO_PK},
