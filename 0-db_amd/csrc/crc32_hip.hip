@@ -87,6 +87,13 @@ constexpr uint64_t DYN_MAX_CHUNKS_PER_RECORD = 64;
 // faster than the small shape for records of 64 B - 2 KiB, 3 % slower at
 // 4 KiB (profiles/r3/ab_packed_sizes.jsonl)
 [[maybe_unused]] constexpr uint64_t TINY_RECORD_MAX = 2048;
+// ... in rows of 8 lanes (eight records per wave) up to 1 KiB and of 4 lanes
+// (sixteen per wave) up to 256 B: every packet then takes one superstep, and
+// more records share its per-packet work (Zipf <= 1 KiB -8 %, Zipf <= 512 B
+// -31 %, Zipf <= 256 B -55 %, 64 B records -71 % against rows of 16;
+// profiles/r3/ab_packed_row_width*.jsonl)
+[[maybe_unused]] constexpr uint64_t TINY8_RECORD_MAX = 1024;
+[[maybe_unused]] constexpr uint64_t TINY4_RECORD_MAX = 256;
 // record-relative grids of records this long load from the dword below the
 // record and fold its last bytes in at the end (next_seg_batched): the fold
 // waits for one dword load at the record's end, which small records cannot
@@ -392,6 +399,8 @@ struct PlanArgs {
     uint32_t lg;
     const uint32_t *bmax; // nb block maxima of a record's unit count (tail-pool guard)
     const uint64_t *dn;   // nullptr, or the record count in device memory (n is then its bound)
+    uint32_t cls_max;     // packed kernel of a split batch: only records of at most this many bytes are its
+                          // (the others -- no units in its plan -- belong to the main kernel); 0: all
 };
 
 __device__ __forceinline__ uint32_t wave_max(uint32_t x) {
@@ -1019,7 +1028,8 @@ __device__ __forceinline__ uint32_t row_pick(uint32_t lane, uint32_t a, uint32_t
     const uint32_t g = lane >> 4;
     return g == 0 ? a : g == 1 ? b : g == 2 ? c : d;
 }
-__device__ __forceinline__ uint64_t row_pick64(uint32_t lane, uint64_t a, uint64_t b, uint64_t c, uint64_t d) {
+__device__ __forceinline__ __attribute__((unused)) uint64_t row_pick64(uint32_t lane, uint64_t a, uint64_t b, uint64_t c,
+                                                                       uint64_t d) {
     const uint32_t g = lane >> 4;
     return g == 0 ? a : g == 1 ? b : g == 2 ? c : d;
 }
@@ -1104,12 +1114,15 @@ __device__ __forceinline__ uint32_t max_rows(uint32_t v) {
 // table image (`dummy`), so that the loads of its empty positions -- which
 // read piece 0's address, F0 = pb + 16 (kb - l16) -- stay inside mapped memory
 // even for an empty record at the very end of the arena.
+// bit of PkGeo::fl: the row holds no record of this kernel (past the range,
+// or a record of the main kernel in a split batch): nothing is stored
+constexpr uint32_t PK_NOSTORE = 1u << 24;
 template <bool VM, int RW = 16>
 __device__ __forceinline__ void pk_geometry(uint64_t A, uint32_t L, uint64_t r0, uint64_t rb, uint32_t lane,
-                                            const uint32_t *dummy, PkGeo &g, PkPacket &p) {
+                                            const uint32_t *dummy, uint32_t cls_max, PkGeo &g, PkPacket &p) {
     using R = PkRow<RW>;
     const uint64_t rg = r0 + lane / RW;
-    const bool valid = rg < rb;
+    const bool valid = rg < rb && (cls_max == 0 || L <= cls_max);
     if (!valid)
         L = 0;
     const uint64_t E = A + L;
@@ -1147,7 +1160,7 @@ __device__ __forceinline__ void pk_geometry(uint64_t A, uint32_t L, uint64_t r0,
     const uint64_t Eg = np ? Ep : reinterpret_cast<uint64_t>(dummy); // then F0 = the table image
     g.pb = Eg - 16ull * R::PPS * S + 16ull * (lane % RW);
     g.kb = kb;
-    g.fl = lo0 | (h << 4) | (d << 8) | (((uint32_t)Ep & 3u) << 16);
+    g.fl = lo0 | (h << 4) | (d << 8) | (((uint32_t)Ep & 3u) << 16) | (valid ? 0u : PK_NOSTORE);
 }
 
 // piece 0 of a row: the rare shifted load (d: the block holding A, moved up
@@ -1356,6 +1369,11 @@ __global__ __launch_bounds__(WGT, WPE) void crc_packed_kernel(
     const bool dyn = DYN > 0 && gridDim.x >= DYN_POOLS && total >= DYN_MIN_UNITS_PER_WAVE * max_waves;
     const uint64_t Ts = dyn ? total - total * DYN / 16 : total;
     const uint32_t *const dummy = tables;
+    if (total == 0) { // nothing of this kernel's in the batch (a split batch without small records)
+        if (blockIdx.x == 0 && threadIdx.x < DYN_MAX_POOLS)
+            scratch[SCRATCH_DYN_CTR + (((epoch + 1u) & 1u) * DYN_MAX_POOLS + threadIdx.x) * 32u] = 0u;
+        return;
+    }
 
     // the wave's first range: the records of its static slice (found before
     // the table fill, so that the search's round trips overlap it)
@@ -1435,7 +1453,7 @@ __global__ __launch_bounds__(WGT, WPE) void crc_packed_kernel(
         const uint64_t ab = reinterpret_cast<uint64_t>(arena);
         PkGeo gc;
         PkPacket pc;
-        pk_geometry<VM, RW>(pk_addr<VM>(m, ab, lane), pk_len<VM>(m, lane), r0, rb, lane, dummy, gc, pc);
+        pk_geometry<VM, RW>(pk_addr<VM>(m, ab, lane), pk_len<VM>(m, lane), r0, rb, lane, dummy, plan.cls_max, gc, pc);
         uint4 cur[K], nxt[K];
         // the loads of superstep s of packet (g, p); with its first superstep,
         // the descriptors of the packet after it (scalar)
@@ -1460,7 +1478,7 @@ __global__ __launch_bounds__(WGT, WPE) void crc_packed_kernel(
                     __builtin_amdgcn_s_waitcnt(0x0F70);
                 if (newp) {
                     pk_geometry<VM, RW>(pk_addr<VM>(m, ab, lane), pk_len<VM>(m, lane), pc.r0 + NR, rb, lane, dummy,
-                                        gn, pn);
+                                        plan.cls_max, gn, pn);
                     issue(gn, pn, 0, nxt);
                 } else {
                     issue(gc, pc, nss, nxt);
@@ -1477,7 +1495,7 @@ __global__ __launch_bounds__(WGT, WPE) void crc_packed_kernel(
             if (newp) {
                 x = pk_finish<VM, RW>(gc, pc, acc, lane, lds);
                 acc = 0;
-                if (lane / RW < pc.nr)
+                if (lane / RW < pc.nr && !(gc.fl & PK_NOSTORE))
                     dst = out + pc.r0 + lane / RW;
             }
             if (lane % RW == 0)
@@ -1507,6 +1525,29 @@ struct KernelVariant {
     int wgs_per_cu = WG_PER_CU;
     uint32_t unit_ovh = UNIT_OVH; // must match the kernel's UO
 };
+
+// batches of records <= 2 KiB: the packed kernel (512 threads: the 768-thread
+// build spills, profiles/r3/ab_packed_kernel.jsonl) with vector-loaded
+// descriptors and fold dwords and one superstep of loads in flight
+// (fixed 2 KiB -16 %, Zipf <= 2 KiB -13 %, 256 B records -23 % against the
+// scalar-loaded first version, profiles/r3/ab_packed_vm*.jsonl)
+const KernelVariant kTiny = {"pk_wg512_dyn4c4p32_sp_wait_vm", crc_packed_kernel<512, 4, 4, 4, 32, true, 1, true, true>,
+                             512, WG_PER_CU, UO_PK};
+const KernelVariant kTiny8 = {"pk8_wg512_dyn4c4p32_sp_wait_vm",
+                              crc_packed_kernel<512, 4, 4, 4, 32, true, 1, true, true, 8>, 512, WG_PER_CU, UO_PK};
+const KernelVariant kTiny4 = {"pk4_wg512_dyn4c4p32_sp_wait_vm",
+                              crc_packed_kernel<512, 4, 4, 4, 32, true, 1, true, true, 4>, 512, WG_PER_CU, UO_PK};
+// Diagnostic library only (A/B): a batch without a known bound split by
+// record size -- records of at most `split` bytes to the packed kernel, the
+// rest to the main kernel, planned in one planner launch (two unit prefixes,
+// a record has units in one of them) and run back to back on the stream.
+// Measured and not shipped: C3's main kernel gets 1.8 %
+// faster without its 57,822 records of <= 1 KiB, but their packed launch
+// takes 39 us and the step goes 0.727 -> 0.749 ms
+// (profiles/r3/ab_split_small_records.jsonl).
+const KernelVariant &split_variant(uint32_t split) {
+    return split <= TINY4_RECORD_MAX ? kTiny4 : split <= TINY8_RECORD_MAX ? kTiny8 : kTiny;
+}
 
 #ifdef ZDBCRC_DIAG
 // diagnostic library only (libzdbcrc_diag.so, scripts/ab.py): A/B variants,
@@ -1587,6 +1628,9 @@ const KernelVariant kVariants[] = {
 };
 constexpr int kNumVariants = (int)(sizeof(kVariants) / sizeof(kVariants[0]));
 std::atomic<int> g_variant{-1};
+// A/B: split unbounded batches at this many bytes (0: never; zdbcrc_debug_set_split)
+std::atomic<uint32_t> g_debug_split{0};
+uint32_t split_bytes(const KernelVariant &) { return g_debug_split.load(); }
 std::atomic<int> g_host_mode{0};
 
 const KernelVariant &variant(uint64_t /*max_len: the A/B harness picks by index*/ = 0) {
@@ -1623,17 +1667,16 @@ const KernelVariant kSmall = {"v3_wg768_nt_dyn4c4p32_sp_pp_wait_bmg_xp",
                               crc_batch_kernel_v3<768, 6, false, 0, UNIT_OVH, false, true, false, 0, 4, 4, 32, true, 3,
                                                   false, true, true>,
                               768};
-// batches of records <= 2 KiB: the packed kernel (512 threads: the 768-thread
-// build spills, profiles/r3/ab_packed_kernel.jsonl) with vector-loaded
-// descriptors and fold dwords and one superstep of loads in flight
-// (fixed 2 KiB -16 %, Zipf <= 2 KiB -13 %, 256 B records -23 % against the
-// scalar-loaded first version, profiles/r3/ab_packed_vm*.jsonl)
-const KernelVariant kTiny = {"pk_wg512_dyn4c4p32_sp_wait_vm", crc_packed_kernel<512, 4, 4, 4, 32, true, 1, true, true>,
-                             512, WG_PER_CU, UO_PK};
+// the product never splits a batch (diagnostic A/B only)
+constexpr uint32_t split_bytes(const KernelVariant &) { return 0u; }
 // the kernel for a batch whose records are at most max_len bytes (0: unknown)
 const KernelVariant &variant(uint64_t max_len = 0) {
     if (max_len == 0 || max_len > SMALL_RECORD_MAX)
         return kDefault;
+    if (max_len <= TINY4_RECORD_MAX)
+        return kTiny4;
+    if (max_len <= TINY8_RECORD_MAX)
+        return kTiny8;
     return max_len <= TINY_RECORD_MAX ? kTiny : kSmall;
 }
 #endif
@@ -1662,64 +1705,99 @@ struct UnitCount {
 // last block) and each block's total (bsum); zeroes out[] on the way (cut
 // records are finished by atomic XOR).  The checksum kernel scans the <= 1024
 // block totals itself, so there is no grid-wide dependency here.
+// SPLIT: two plans at once -- records of more than `split` bytes for the main
+// kernel (ovh per record), the others for the packed kernel (ovh_s); a
+// record has units in one plan only.
 constexpr uint32_t PLAN_T = 256;
+struct PlanOut {
+    uint64_t *local;
+    uint64_t *bsum;
+    uint32_t *bmax;
+};
 
+template <bool SPLIT>
+__device__ __forceinline__ uint64_t plan_units(const uint8_t *arena, const uint64_t *offsets, uint32_t L, uint64_t r,
+                                               uint64_t ovh, bool mine) {
+    if (!mine)
+        return 0;
+    uint64_t v = ovh;
+    if (L) {
+        const uint64_t a = reinterpret_cast<uint64_t>(arena) + offsets[r];
+        v += record_pieces(a, L);
+    }
+    return v;
+}
+
+template <bool SPLIT>
 __global__ __launch_bounds__(PLAN_T) void plan_kernel(const uint8_t *__restrict__ arena,
                                                       const uint64_t *__restrict__ offsets,
                                                       const uint32_t *__restrict__ lengths, uint64_t n, uint64_t ovh,
-                                                      uint32_t lg, uint64_t *__restrict__ local,
-                                                      uint64_t *__restrict__ bsum, uint32_t *__restrict__ bmax,
-                                                      uint32_t *__restrict__ out, const uint64_t *__restrict__ dn) {
+                                                      uint32_t lg, PlanOut pb, uint32_t *__restrict__ out,
+                                                      const uint64_t *__restrict__ dn, uint32_t split, uint64_t ovh_s,
+                                                      PlanOut ps) {
     if (dn) { // device-side record count, n its bound (records past it: no units)
         const uint64_t m = *dn;
         n = m < n ? m : n;
     }
     __shared__ uint64_t wsum[2 * (PLAN_T / 64) + 1];
-    __shared__ uint32_t wmx[PLAN_T / 64];
-    uint32_t mx = 0;
+    __shared__ uint32_t wmx[2][PLAN_T / 64];
+    uint32_t mx = 0, mxs = 0;
     const uint32_t per = (1u << lg) / PLAN_T;
     const uint64_t r0 = ((uint64_t)blockIdx.x << lg) + (uint64_t)threadIdx.x * per;
-    uint64_t s = 0;
+    uint64_t s = 0, ss = 0;
     for (uint32_t i = 0; i < per; i++) {
         const uint64_t r = r0 + i;
         if (r < n) {
             const uint32_t L = lengths[r];
-            uint64_t v = ovh;
-            if (L) {
-                const uint64_t a = reinterpret_cast<uint64_t>(arena) + offsets[r];
-                v += record_pieces(a, L);
-            }
+            const bool small = SPLIT && L <= split;
+            const uint64_t v = plan_units<SPLIT>(arena, offsets, L, r, ovh, !small);
             s += v;
             mx = v > mx ? (uint32_t)v : mx;
+            if (SPLIT) {
+                const uint64_t vs = plan_units<SPLIT>(arena, offsets, L, r, ovh_s, small);
+                ss += vs;
+                mxs = vs > mxs ? (uint32_t)vs : mxs;
+            }
             out[r] = 0;
         }
     }
     mx = wave_max(mx);
-    if ((threadIdx.x & 63u) == 0)
-        wmx[threadIdx.x >> 6] = mx;
-    uint64_t total;
+    if (SPLIT)
+        mxs = wave_max(mxs);
+    if ((threadIdx.x & 63u) == 0) {
+        wmx[0][threadIdx.x >> 6] = mx;
+        wmx[1][threadIdx.x >> 6] = mxs;
+    }
+    uint64_t total, total_s = 0;
     uint64_t e = block_excl_scan64<PLAN_T>(s, wsum, &total); // its barriers publish wmx
+    uint64_t es = SPLIT ? block_excl_scan64<PLAN_T>(ss, wsum, &total_s) : 0;
     for (uint32_t i = 0; i < per; i++) {
         const uint64_t r = r0 + i;
         if (r > n)
             break;
-        local[r] = e;
+        pb.local[r] = e;
+        if (SPLIT)
+            ps.local[r] = es;
         if (r < n) {
             const uint32_t L = lengths[r];
-            uint64_t v = ovh;
-            if (L) {
-                const uint64_t a = reinterpret_cast<uint64_t>(arena) + offsets[r];
-                v += record_pieces(a, L);
-            }
-            e += v;
+            const bool small = SPLIT && L <= split;
+            e += plan_units<SPLIT>(arena, offsets, L, r, ovh, !small);
+            if (SPLIT)
+                es += plan_units<SPLIT>(arena, offsets, L, r, ovh_s, small);
         }
     }
     if (threadIdx.x == 0) {
-        bsum[blockIdx.x] = total;
-        uint32_t m = 0;
-        for (uint32_t i = 0; i < PLAN_T / 64; i++)
-            m = wmx[i] > m ? wmx[i] : m;
-        bmax[blockIdx.x] = m;
+        uint32_t m = 0, ms = 0;
+        for (uint32_t i = 0; i < PLAN_T / 64; i++) {
+            m = wmx[0][i] > m ? wmx[0][i] : m;
+            ms = wmx[1][i] > ms ? wmx[1][i] : ms;
+        }
+        pb.bsum[blockIdx.x] = total;
+        pb.bmax[blockIdx.x] = m;
+        if (SPLIT) {
+            ps.bsum[blockIdx.x] = total_s;
+            ps.bmax[blockIdx.x] = ms;
+        }
     }
 }
 
@@ -1980,6 +2058,7 @@ struct DeviceCtx {
 struct TimedLaunch {
     int dev;
     hipEvent_t e0, e1;
+    int kind; // 0: the main kernel; 1: the packed kernel of a split batch
 };
 
 // Locking: one mutex per device serialises that device's context,
@@ -1993,8 +2072,8 @@ DeviceCtx g_dev[64];
 std::atomic<bool> g_hip_touched{false};
 std::atomic<bool> g_timing{false};
 std::vector<TimedLaunch> g_pending;
-double g_time_ms = 0;
-uint64_t g_launches = 0;
+double g_time_ms[2] = {0, 0};
+uint64_t g_launches[2] = {0, 0};
 std::vector<hipEvent_t> g_event_pool[64]; // events are reused on the device they were created on
 #ifdef ZDBCRC_DIAG
 uint32_t *g_last_scratch = nullptr; // STAMP read-back (single-threaded measurement scripts)
@@ -2059,13 +2138,18 @@ int enqueue_batch(int dev, DeviceCtx &c, const KernelVariant &kv, const uint8_t 
     while (((n + 1 + (1ull << lg) - 1) >> lg) > PLAN_MAX_BLOCKS)
         lg++;
     const uint64_t nb = (n + 1 + (1ull << lg) - 1) >> lg;
+    // an unbounded, device-planned batch is split by record size (SPLIT_BYTES):
+    // the packed kernel takes the small records, then kv the others
+    const uint32_t split = d_unit_start ? 0u : split_bytes(kv);
+    const int nplans = split ? 2 : 1;
     auto al = [](size_t x) { return (x + 255) & ~size_t(255); };
     const size_t local_bytes = d_unit_start ? 0 : al((n + 1) * sizeof(uint64_t));
     const size_t bsum_bytes = d_unit_start ? 0 : al(nb * sizeof(uint64_t));
     const size_t bmax_bytes = d_unit_start ? 0 : al(nb * sizeof(uint32_t));
+    const size_t plan_bytes = local_bytes + bsum_bytes + bmax_bytes;
     // dummy dword per wave (64 KiB) | diagnostic stamps (448 KiB) | per-CU counters (4 KiB) | DYN counters (16 KiB)
     const size_t scratch_bytes = (64 + 448 + 4 + 16) * 1024;
-    const size_t need = scratch_bytes + local_bytes + bsum_bytes + bmax_bytes;
+    const size_t need = scratch_bytes + nplans * plan_bytes;
     Workspace &w = c.ws[reinterpret_cast<void *>(st)];
     if (w.bytes < need) {
         if (w.ptr) {
@@ -2085,17 +2169,29 @@ int enqueue_batch(int dev, DeviceCtx &c, const KernelVariant &kv, const uint8_t 
 #ifdef ZDBCRC_DIAG
     g_last_scratch = scratch;
 #endif
-    PlanArgs plan{d_unit_start, nullptr, 0, 0, nullptr, d_n};
+    PlanArgs plan{d_unit_start, nullptr, 0, 0, nullptr, d_n, 0};
+    PlanArgs plan_s{};
+    [[maybe_unused]] const KernelVariant &ks = split_variant(split ? split : 1);
     if (!d_unit_start) {
-        uint8_t *base = static_cast<uint8_t *>(w.ptr) + scratch_bytes;
-        uint64_t *local = reinterpret_cast<uint64_t *>(base);
-        uint64_t *bsum = reinterpret_cast<uint64_t *>(base + local_bytes);
-        uint32_t *bmax = reinterpret_cast<uint32_t *>(base + local_bytes + bsum_bytes);
-        hipLaunchKernelGGL(plan_kernel, dim3((uint32_t)nb), dim3(PLAN_T), 0, st, arena, offsets, lengths, n,
-                           (uint64_t)kv.unit_ovh, lg, local, bsum, bmax, out, d_n);
+        PlanOut po[2];
+        for (int k = 0; k < nplans; k++) {
+            uint8_t *base = static_cast<uint8_t *>(w.ptr) + scratch_bytes + k * plan_bytes;
+            po[k] = PlanOut{reinterpret_cast<uint64_t *>(base), reinterpret_cast<uint64_t *>(base + local_bytes),
+                            reinterpret_cast<uint32_t *>(base + local_bytes + bsum_bytes)};
+        }
+#ifdef ZDBCRC_DIAG
+        if (split)
+            hipLaunchKernelGGL(plan_kernel<true>, dim3((uint32_t)nb), dim3(PLAN_T), 0, st, arena, offsets, lengths, n,
+                               (uint64_t)kv.unit_ovh, lg, po[0], out, d_n, split, (uint64_t)ks.unit_ovh, po[1]);
+        else
+#endif
+            hipLaunchKernelGGL(plan_kernel<false>, dim3((uint32_t)nb), dim3(PLAN_T), 0, st, arena, offsets, lengths,
+                               n, (uint64_t)kv.unit_ovh, lg, po[0], out, d_n, 0u, (uint64_t)0, po[0]);
         if (hipGetLastError() != hipSuccess)
             return ZDB_CRC32_ELAUNCH;
-        plan = PlanArgs{local, bsum, (uint32_t)nb, lg, bmax, d_n};
+        plan = PlanArgs{po[0].local, po[0].bsum, (uint32_t)nb, lg, po[0].bmax, d_n, 0};
+        if (split)
+            plan_s = PlanArgs{po[1].local, po[1].bsum, (uint32_t)nb, lg, po[1].bmax, d_n, split};
     } else if (!out_zeroed && hipMemsetAsync(out, 0, n * sizeof(uint32_t), st) != hipSuccess) {
         return ZDB_CRC32_ELAUNCH;
     }
@@ -2107,31 +2203,53 @@ int enqueue_batch(int dev, DeviceCtx &c, const KernelVariant &kv, const uint8_t 
     if (grid_wgs && grid_wgs < grid)
         grid = grid_wgs;
     const uint32_t max_waves = grid * (uint32_t)(kv.threads / 64);
-    hipEvent_t e0 = nullptr, e1 = nullptr;
+    hipEvent_t e0 = nullptr, e1 = nullptr, e2 = nullptr, e3 = nullptr; // main kernel; packed kernel (split)
     std::unique_lock<std::mutex> tl(g_mu, std::defer_lock);
     if (g_timing.load()) {
         tl.lock();
         std::vector<hipEvent_t> &pool = g_event_pool[dev];
-        for (hipEvent_t *e : {&e0, &e1}) {
-            if (!pool.empty()) {
-                *e = pool.back();
-                pool.pop_back();
-            } else if (hipEventCreate(e) != hipSuccess) {
-                *e = nullptr;
+        // a pair of events, or none (no timing for a launch rather than a half-bracketed one)
+        auto take = [&](hipEvent_t &a, hipEvent_t &b) {
+            for (hipEvent_t *e : {&a, &b}) {
+                if (!pool.empty()) {
+                    *e = pool.back();
+                    pool.pop_back();
+                } else if (hipEventCreate(e) != hipSuccess) {
+                    *e = nullptr;
+                }
             }
-        }
-        if (!e0 || !e1) { // no timing for this launch rather than a half-bracketed one
-            for (hipEvent_t e : {e0, e1})
-                if (e)
-                    pool.push_back(e);
-            e0 = e1 = nullptr;
-        }
+            if (!a || !b) {
+                for (hipEvent_t e : {a, b})
+                    if (e)
+                        pool.push_back(e);
+                a = b = nullptr;
+            }
+        };
+        take(e0, e1);
+        if (split)
+            take(e2, e3);
     }
     // the launch counter picks the tail-pool counter parity; it advances only
     // when a kernel was enqueued (each launch clears the next parity's counters)
-    const uint32_t ep = w.launches + 1;
+    uint32_t ep = w.launches + 1;
     // timing: the dispatch packet itself carries the start/stop events
-    // (hipExtLaunchKernel), so no marker packets sit between the kernels
+    // (hipExtLaunchKernel), so no marker packets sit between the kernels;
+    // the packed kernel of a split batch has its own pair (kind 1)
+#ifdef ZDBCRC_DIAG
+    if (split) {
+        const uint32_t sgrid = (uint32_t)(c.cus * ks.wgs_per_cu);
+        const uint32_t swaves = sgrid * (uint32_t)(ks.threads / 64);
+        if (e2)
+            hipExtLaunchKernelGGL(ks.fn, dim3(sgrid), dim3(ks.threads), 0, st, e2, e3, 0u, arena, offsets,
+                                  lengths, plan_s, n, out, c.d_tables, swaves, scratch, ep);
+        else
+            hipLaunchKernelGGL(ks.fn, dim3(sgrid), dim3(ks.threads), 0, st, arena, offsets, lengths, plan_s, n, out,
+                               c.d_tables, swaves, scratch, ep);
+        if (hipGetLastError() != hipSuccess)
+            return ZDB_CRC32_ELAUNCH;
+        w.launches = ep++;
+    }
+#endif
     if (e0)
         hipExtLaunchKernelGGL(kv.fn, dim3(grid), dim3(kv.threads), 0, st, e0, e1, 0u, arena, offsets, lengths,
                               plan, n, out, c.d_tables, max_waves, scratch, ep);
@@ -2142,7 +2260,9 @@ int enqueue_batch(int dev, DeviceCtx &c, const KernelVariant &kv, const uint8_t 
         return ZDB_CRC32_ELAUNCH;
     w.launches = ep;
     if (e1)
-        g_pending.push_back(TimedLaunch{dev, e0, e1});
+        g_pending.push_back(TimedLaunch{dev, e0, e1, 0});
+    if (e3)
+        g_pending.push_back(TimedLaunch{dev, e2, e3, 1});
     return ZDB_CRC32_OK;
 }
 
@@ -2335,6 +2455,12 @@ int zdbcrc_debug_read_stamps(uint64_t *host, size_t waves) {
 
 // measurement hook (not part of the public ABI): select a kernel variant for
 // A/B timing in one process; returns its name, NULL if out of range
+// A/B: split unbounded batches at this many bytes (0: never)
+int zdbcrc_debug_set_split(uint32_t bytes) {
+    g_debug_split.store(bytes);
+    return 0;
+}
+
 const char *zdbcrc_debug_set_variant(int idx) {
     if (idx < 0 || idx >= kNumVariants)
         return nullptr;
@@ -2679,9 +2805,9 @@ static int drain_timing(float *each, size_t max_each, size_t *n_each) {
             return ZDB_CRC32_ELAUNCH;
         float ms = 0;
         hipEventElapsedTime(&ms, p.e0, p.e1);
-        g_time_ms += ms;
-        g_launches += 1;
-        if (each && k < max_each)
+        g_time_ms[p.kind] += ms;
+        g_launches[p.kind] += 1;
+        if (each && k < max_each && p.kind == 0)
             each[k++] = ms;
         g_event_pool[p.dev].push_back(p.e0);
         g_event_pool[p.dev].push_back(p.e1);
@@ -2699,25 +2825,34 @@ long zdbcrc_debug_kernel_times(float *each, size_t max_each) {
     size_t k = 0;
     if (drain_timing(each, max_each, &k))
         return -1;
-    g_time_ms = 0;
-    g_launches = 0;
+    g_time_ms[0] = g_time_ms[1] = 0;
+    g_launches[0] = g_launches[1] = 0;
     return (long)k;
 }
 
 #endif // ZDBCRC_DIAG
 
-int zdb_crc32_kernel_stats(double *total_ms, uint64_t *launches) {
+static int kernel_stats_of(int kind, double *total_ms, uint64_t *launches) {
     std::lock_guard<std::mutex> g(g_mu);
     if (int rc = drain_timing(nullptr, 0, nullptr))
         return rc;
     if (total_ms)
-        *total_ms = g_time_ms;
+        *total_ms = g_time_ms[kind];
     if (launches)
-        *launches = g_launches;
-    g_time_ms = 0;
-    g_launches = 0;
+        *launches = g_launches[kind];
+    g_time_ms[kind] = 0;
+    g_launches[kind] = 0;
     return ZDB_CRC32_OK;
 }
+
+int zdb_crc32_kernel_stats(double *total_ms, uint64_t *launches) { return kernel_stats_of(0, total_ms, launches); }
+
+#ifdef ZDBCRC_DIAG
+// debug: the packed kernel of split batches (A/B of zdbcrc_debug_set_split)
+int zdbcrc_debug_small_kernel_stats(double *total_ms, uint64_t *launches) {
+    return kernel_stats_of(1, total_ms, launches);
+}
+#endif
 
 // ---------------------------------------------------------------------------
 // f1: host -> device ingest stream (include/zdb_crc32.h, section 2b)

@@ -15,9 +15,20 @@ import torch, zdbcrc
 sys.path.insert(0, str(ROOT))
 import bench
 
-set_variant = zdbcrc._lib.zdbcrc_debug_set_variant
-set_variant.restype = C.c_char_p
-set_variant.argtypes = [C.c_int]
+set_variant_raw = zdbcrc._lib.zdbcrc_debug_set_variant
+set_variant_raw.restype = C.c_char_p
+set_variant_raw.argtypes = [C.c_int]
+set_split = zdbcrc._lib.zdbcrc_debug_set_split
+set_split.argtypes = [C.c_uint32]
+_small_stats = zdbcrc._lib.zdbcrc_debug_small_kernel_stats
+_small_stats.argtypes = [C.POINTER(C.c_double), C.POINTER(C.c_uint64)]
+
+
+def small_kernel_stats():
+    ms, k = C.c_double(0), C.c_uint64(0)
+    _small_stats(C.byref(ms), C.byref(k))
+    return ms.value, k.value
+set_variant = set_variant_raw
 names = []
 i = 0
 while True:
@@ -40,7 +51,19 @@ for mib in [int(x) for x in os.environ.get("PROBE_MIB", "4096").split(",") if x]
                           "median_ms": round(float(np.median(ts)), 4),
                           "tbs": round(buf.numel() / (np.median(ts) / 1e3) / 1e12, 3)}), flush=True)
     del buf
-sel = [int(x) for x in sys.argv[2].split(",")] if len(sys.argv) > 2 else list(range(len(names)))
+# a variant spec is "<index>" or "<index>s<bytes>": the kernel variant, and
+# unbounded batches split at that many bytes (small records to the packed
+# kernel; the time reported is then both kernels' sum)
+specs = sys.argv[2].split(",") if len(sys.argv) > 2 else [str(i) for i in range(len(names))]
+sel = list(range(len(specs)))
+vidx = [int(x.split("s")[0]) for x in specs]
+vsplit = [int(x.split("s")[1]) if "s" in x else 0 for x in specs]
+vname = [names[vidx[i]] + (f"+split{vsplit[i]}" if vsplit[i] else "") for i in sel]
+
+
+def set_spec(i):
+    set_variant_raw(vidx[i])
+    set_split(vsplit[i])
 work = sys.argv[1] if len(sys.argv) > 1 else "zipf"
 ROUNDS, STEPS = 5, 5
 for wl in [w for w in work.split(",") if w and w != "none"]:
@@ -89,8 +112,9 @@ for wl in [w for w in work.split(",") if w and w != "none"]:
     do, dl = torch.from_numpy(offs).cuda(), torch.from_numpy(lens.astype(np.int32)).cuda()
     outs = {v: torch.empty(len(lens), dtype=torch.int32, device="cuda") for v in sel}
     times = {v: [] for v in sel}
+    walls = {v: [] for v in sel}
     # clock settle: ~1 s of untimed launches before the first timed round
-    set_variant(sel[0])
+    set_spec(sel[0])
     t_end = time.time() + float(os.environ.get("SETTLE_S", "1.0"))
     while time.time() < t_end:
         for _ in range(20):
@@ -98,19 +122,24 @@ for wl in [w for w in work.split(",") if w and w != "none"]:
         torch.cuda.synchronize()
     for r in range(ROUNDS):
         for v in sel:
-            set_variant(v)
+            set_spec(v)
             zdbcrc.batch_device(arena, do, dl, outs[v])
-            torch.cuda.synchronize(); zdbcrc.kernel_stats(); zdbcrc.set_timing(True)
+            torch.cuda.synchronize(); zdbcrc.kernel_stats(); small_kernel_stats(); zdbcrc.set_timing(True)
+            t0 = time.perf_counter()
             for _ in range(STEPS):
                 zdbcrc.batch_device(arena, do, dl, outs[v])
-            torch.cuda.synchronize(); zdbcrc.set_timing(False)
-            ms, k = zdbcrc.kernel_stats(); times[v].append(ms / k)
+            torch.cuda.synchronize(); t1 = time.perf_counter(); zdbcrc.set_timing(False)
+            ms, k = zdbcrc.kernel_stats()
+            ms2, k2 = small_kernel_stats()
+            times[v].append(ms / k + (ms2 / k2 if k2 else 0.0))
+            walls[v].append((t1 - t0) / STEPS * 1e3)
     ref = outs[sel[0]].cpu()
     payload = int(lens.sum())
     for v in sel:
         t = np.array(times[v])
         same = bool(torch.equal(outs[v].cpu(), ref))
-        print(json.dumps({"workload": label, "variant": names[v], "median_ms": round(float(np.median(t)), 4),
+        print(json.dumps({"workload": label, "variant": vname[v], "median_ms": round(float(np.median(t)), 4),
+                          "step_ms_median": round(float(np.median(walls[v])), 4),
                           "min_ms": round(float(t.min()), 4),
                           "gibs_median": round(payload / (np.median(t) / 1e3) / 2**30, 1),
                           "frac_spec": round((payload + 16 * len(lens)) / (np.median(t) / 1e3) / 8e12, 4),

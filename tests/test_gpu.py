@@ -679,6 +679,23 @@ def _packed_cases():
     out["hint_too_small"] = (offs, lens, 2048)  # the bound is wrong: still exact
     lens = np.full(1 << 16, 64)
     out["fixed_64B"] = (np.arange(1 << 16, dtype=np.int64) * 64, lens, 64)
+    # narrower rows: bounds <= 256 B take rows of 4 lanes, <= 1 KiB rows of 8
+    for bound in (256, 1024):
+        lens = rng.integers(0, bound + 1, 100_000)
+        offs = np.zeros(len(lens), np.int64)
+        offs[1:] = np.cumsum(lens[:-1] + rng.integers(0, 5, len(lens) - 1))
+        out[f"random_0_{bound}"] = (offs, lens, bound)
+        offs, ls = [], []
+        for p in range(32):
+            for a in range(16):
+                for L in (0, 1, 2, 3, 5, 17, 100, bound - 3, bound):
+                    offs.append(4096 * (p * 4 + 1) + a)
+                    ls.append(L)
+        out[f"page_start_{bound}"] = (np.array(offs), np.array(ls), bound)
+        lens = np.concatenate([rng.integers(0, bound, 3000), [1 << 20, 70_000, bound + 1], rng.integers(0, bound, 3000)])
+        offs = np.zeros(len(lens), np.int64)
+        offs[1:] = np.cumsum(lens[:-1] + 1)
+        out[f"hint_too_small_{bound}"] = (offs, lens, bound)  # a wrong bound: still exact
     return out
 
 
@@ -706,7 +723,7 @@ def test_packed_kernel_small_records(dev, oracle_c, case):
         dev.batch_device(a, o, l, out, max_length=bound)
         torch.cuda.synchronize()
         np.testing.assert_array_equal(out.cpu().numpy().view(np.uint32), want)
-    if lens.max() <= 2048:  # the host entry takes the packed kernel from the lengths themselves
+    if lens.max() <= 2048:  # the host entry takes the packed kernel (its row width) from the lengths themselves
         np.testing.assert_array_equal(dev.batch_host(arena, offs.astype(np.uint64), lens.astype(np.uint32)), want)
 
 
