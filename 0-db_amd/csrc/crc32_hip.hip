@@ -430,6 +430,55 @@ __device__ __forceinline__ uint64_t find_record(const UnitPrefix &unit_start, ui
     return lo;
 }
 
+// the same search through the planner's block structure: the block from the
+// offsets in LDS (two LDS rounds), then the block's records in ONE round of
+// global loads (up to 4 per lane, issued together; the prefix is monotone,
+// so the answer is the count of records at or below b) -- one HBM round trip
+// instead of one per 64-way round (3 for C3's 86,959 records, 4 for 1 M)
+__device__ __forceinline__ uint64_t find_record_blocked(const UnitPrefix &unit_start, uint32_t nb, uint64_t n,
+                                                        uint64_t b, uint32_t lane) {
+    if (!unit_start.boff || nb == 0)
+        return find_record(unit_start, n, b, lane);
+    uint64_t lo = 0, hi = nb; // last block bi with boff[bi] <= b
+    while (hi - lo > 1) {
+        const uint64_t step = (hi - lo + 63) >> 6;
+        const uint64_t idx = lo + (uint64_t)lane * step;
+        const uint64_t mask = __ballot(idx < hi && unit_start.boff[idx] <= b);
+        const uint32_t L = 63u - (uint32_t)__clzll(mask);
+        lo += (uint64_t)L * step;
+        const uint64_t h2 = lo + step;
+        hi = h2 < hi ? h2 : hi;
+    }
+    const uint64_t bo = unit_start.boff[lo];
+    const uint64_t r0 = lo << unit_start.lg;
+    const uint64_t r1 = ((lo + 1) << unit_start.lg) < n ? ((lo + 1) << unit_start.lg) : n;
+    const uint64_t q = (r1 - r0 + 63) >> 6;
+    if (q > 4) { // blocks of more than 256 records: 64-way rounds inside the block
+        uint64_t a = r0, z = r1;
+        while (z - a > 1) {
+            const uint64_t step = (z - a + 63) >> 6;
+            const uint64_t idx = a + (uint64_t)lane * step;
+            const uint64_t mask = __ballot(idx < z && unit_start.local[idx] + bo <= b);
+            const uint32_t L = 63u - (uint32_t)__clzll(mask);
+            a += (uint64_t)L * step;
+            const uint64_t h2 = a + step;
+            z = h2 < z ? h2 : z;
+        }
+        return a;
+    }
+    uint64_t v[4];
+#pragma unroll
+    for (uint32_t k = 0; k < 4; k++) {
+        const uint64_t idx = r0 + 64u * k + lane;
+        v[k] = k < q && idx < r1 ? unit_start.local[idx] : ~0ull;
+    }
+    uint32_t cnt = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < 4; k++)
+        cnt += (uint32_t)__popcll(__ballot(v[k] != ~0ull && v[k] + bo <= b));
+    return r0 + cnt - 1;
+}
+
 // metadata of 64 consecutive records [rb, rb+64), record rb+l on lane l
 struct MetaBatch {
     uint64_t rb;   // uniform
@@ -619,7 +668,7 @@ __device__ __forceinline__ uint64_t block_excl_scan64(uint64_t v, uint64_t *wsum
 template <int WGT, int WPE, bool STAMP = false, int PRIO = 0, uint32_t UO = UNIT_OVH, int NOZ = 0,
           bool NTL = false, bool NOLOAD = false, int XM = 0, int DYN = 0, int CPW = 4, uint32_t DYN_POOLS = 8,
           bool SP = false, int PP = 0, bool SEGDUMP = false, bool BMG = false, bool XP = false,
-          uint64_t DWGM = DWG_MIN_BYTES>
+          uint64_t DWGM = DWG_MIN_BYTES, bool FRB = false>
 __global__ __launch_bounds__(WGT, WPE) void crc_batch_kernel_v3(
     const uint8_t *__restrict__ arena, const uint64_t *__restrict__ offsets,
     const uint32_t *__restrict__ lengths, const PlanArgs plan, uint64_t n,
@@ -707,7 +756,7 @@ __global__ __launch_bounds__(WGT, WPE) void crc_batch_kernel_v3(
     Seg cur, nx;
     uint4 bufc[K], bufn[K];
     if (active) {
-        rn = find_record(unit_start, n, ub, lane);
+        rn = FRB ? find_record_blocked(unit_start, plan.nb, n, ub, lane) : find_record(unit_start, n, ub, lane);
         load_meta(m, rn, n, lane, unit_start, arena, offsets, lengths);
         active = next_seg_batched<UO, BMG, DWGM>(rn, n, ub, ue, lane, m, unit_start, arena, offsets, lengths, cur);
         if (active)
@@ -777,7 +826,7 @@ __global__ __launch_bounds__(WGT, WPE) void crc_batch_kernel_v3(
             ue = P0 + PL * (c + 1) / nch;
             if (ue <= ub)
                 continue;
-            rn = find_record(unit_start, n, ub, lane);
+            rn = FRB ? find_record_blocked(unit_start, plan.nb, n, ub, lane) : find_record(unit_start, n, ub, lane);
             if (rn < m.rb)
                 load_meta(m, rn, n, lane, unit_start, arena, offsets, lengths);
             if (next_seg_batched<UO, BMG, DWGM>(rn, n, ub, ue, lane, m, unit_start, arena, offsets, lengths, sg))
@@ -1619,6 +1668,9 @@ const KernelVariant kVariants[] = {
     // is a global (not flat) load -- small shape and default
     {"v3_wg768_nt_dyn4c4p32_sp_pp_wait_dwg0_xp", crc_batch_kernel_v3<768, 6, false, 0, UNIT_OVH, false, true, false, 0, 4, 4, 32, true, 3, false, false, true, 0>, 768},
     {"v3_wg768_nt_dyn4c4p32_sp_dwg0_xp", crc_batch_kernel_v3<768, 6, false, 0, UNIT_OVH, false, true, false, 0, 4, 4, 32, true, 0, false, false, true, 0>, 768},
+    // round 3 (resumed): record search through the planner's blocks (one HBM round trip per search)
+    {"v3_wg768_nt_dyn4c4p32_sp_xp_frb", crc_batch_kernel_v3<768, 6, false, 0, UNIT_OVH, false, true, false, 0, 4, 4, 32, true, 0, false, false, true, DWG_MIN_BYTES, true>, 768},
+    {"v3_wg768_nt_dyn4c4p32_sp_pp_wait_bmg_xp_frb", crc_batch_kernel_v3<768, 6, false, 0, UNIT_OVH, false, true, false, 0, 4, 4, 32, true, 3, false, true, true, DWG_MIN_BYTES, true>, 768},
     // rows of 8 and 4 lanes (8 / 16 records per wave)
     {"pk8_wg512_dyn4c4p32_sp_wait_vm", crc_packed_kernel<512, 4, 4, 4, 32, true, 1, true, true, 8>, 512, WG_PER_CU, UO_PK},
     {"pk4_wg512_dyn4c4p32_sp_wait_vm", crc_packed_kernel<512, 4, 4, 4, 32, true, 1, true, true, 4>, 512, WG_PER_CU, UO_PK},
