@@ -84,9 +84,10 @@ int zdb_crc32_batch_device(const uint8_t *d_arena, const uint64_t *d_offsets,
 /* As zdb_crc32_batch_device, for a caller that knows an upper bound of its
  * record lengths (max_length, 0 = unknown): batches of records <= 4 KiB
  * (fixed-size values, pipelined small SETs) take the small-record loop shape
- * of the kernel, batches of records <= 2 KiB the packed kernel (four records
- * per wave).  Exact for any input; a record longer than the bound only costs
- * speed.  The host-buffer entry points measure the bound themselves. */
+ * of the kernel, batches of records <= 2 KiB / 1 KiB / 256 B the packed
+ * kernel (4 / 8 / 16 records per wave).  Exact for any input; a record longer
+ * than the bound only costs speed.  The host-buffer entry points measure the
+ * bound themselves. */
 int zdb_crc32_batch_device_sized(const uint8_t *d_arena, const uint64_t *d_offsets,
                                  const uint32_t *d_lengths, uint32_t *d_out,
                                  size_t n, uint32_t max_length, void *stream);
