@@ -265,6 +265,38 @@ def test_full_size_small_record_digests(dev, oracle_c, digests, workload, max_le
     del arena
 
 
+@pytest.mark.parametrize("bound", [256, 1024, 2048])
+def test_packed_shapes_at_scale(dev, oracle_c, bound):
+    """each packed shape (rows of 4 / 8 / 16 lanes) on 512 MiB of C3's own
+    record sizes up to its bound (Zipf, tiled; records at every alignment):
+    equal to the default kernel on every record, and to the oracle on a
+    sample of 20,000 records spread over the batch"""
+    base = dev.zipf_lengths(4 << 30, 0xC3C3C3).astype(np.int64)
+    base = base[base <= bound]
+    size = 512 << 20
+    lens = np.tile(base, -(-size // int(base.sum())))
+    lens = lens[:int(np.searchsorted(np.cumsum(lens), size))]
+    rng = np.random.default_rng(bound)
+    offs = np.zeros(len(lens), np.int64)
+    offs[1:] = np.cumsum(lens[:-1] + rng.integers(0, 4, len(lens) - 1))
+    total = int(offs[-1] + lens[-1])
+    arena = torch.empty(total + 64, dtype=torch.uint8, device="cuda")
+    dev.synth_fill_device(arena[:total], 0x5EED + bound)
+    o = torch.from_numpy(offs).cuda()
+    l = torch.from_numpy(lens.astype(np.int32)).cuda()
+    packed = torch.empty(len(lens), dtype=torch.int32, device="cuda")
+    default = torch.empty(len(lens), dtype=torch.int32, device="cuda")
+    dev.batch_device(arena, o, l, packed, max_length=bound)
+    dev.batch_device(arena, o, l, default)
+    torch.cuda.synchronize()
+    got = packed.cpu().numpy().view(np.uint32)
+    np.testing.assert_array_equal(got, default.cpu().numpy().view(np.uint32))
+    host = dev.synth_fill(total, 0x5EED + bound)
+    pick = np.unique(np.linspace(0, len(lens) - 1, 20_000).astype(np.int64))
+    np.testing.assert_array_equal(got[pick], oracle_c.batch(host, offs[pick], lens[pick]))
+    del arena
+
+
 def test_full_size_c3_digest(dev, oracle_c, digests):
     """C3 at BASELINE size (Zipf 64 B..1 MiB, ~4 GiB, any alignment)."""
     d = digests["C3"]
