@@ -2450,6 +2450,12 @@ float zdbcrc_debug_stream_read(const void *d_buf, size_t bytes, uint32_t *d_sink
         hipLaunchKernelGGL((stream_slice_kernel<4, true>), dim3(512), dim3(1024), 0, st, src, words, d_sink);
     else if (blocks == -204)
         hipLaunchKernelGGL((stream_slice_kernel<4, true>), dim3(512), dim3(768), 0, st, src, words, d_sink);
+    else if (blocks == -202) // 768 threads, 2 / 1 loads in flight per lane (bytes in flight per CU: 48 / 24 KiB)
+        hipLaunchKernelGGL((stream_slice_kernel<2, true>), dim3(512), dim3(768), 0, st, src, words, d_sink);
+    else if (blocks == -201)
+        hipLaunchKernelGGL((stream_slice_kernel<1, true>), dim3(512), dim3(768), 0, st, src, words, d_sink);
+    else if (blocks == -208)
+        hipLaunchKernelGGL((stream_slice_kernel<8, true>), dim3(512), dim3(768), 0, st, src, words, d_sink);
     else if (blocks == -108)
         hipLaunchKernelGGL((stream_slice_kernel<8, true>), dim3(512), dim3(1024), 0, st, src, words, d_sink);
     else if (blocks == -304) // packed access shapes (stream_rows_kernel): rows of 4 / 8 / 16 / 64 lanes
