@@ -81,19 +81,17 @@ constexpr uint64_t DYN_MIN_UNITS_PER_WAVE = 4096;
 // ... and no record spans more than this many chunks (each chunk cut of a
 // record is one same-address atomic XOR: one huge record would serialise them)
 constexpr uint64_t DYN_MAX_CHUNKS_PER_RECORD = 64;
-// records up to this many bytes take the small-record loop shape (PP)
+// batches whose records are known to be at most this many bytes take the
+// packed kernel (crc_packed_kernel, 768 threads, one load buffer): rows of 16
+// lanes up to 4 KiB, of 8 up to 2 KiB, of 4 up to 512 B.  Against the main
+// kernel's small-record loop shape (round 2's choice for <= 4 KiB): C2
+// 0.766 -> 0.709 ms, C2u 0.800 -> 0.780, Zipf <= 4 KiB 3.64 -> 2.06, 2 KiB
+// records 0.939 -> 0.705, Zipf <= 512 B 2.54 -> 0.56
+// (profiles/r3/ab_packed_single_buffer*.jsonl)
 [[maybe_unused]] constexpr uint64_t SMALL_RECORD_MAX = 4096;
-// ... and up to this many the packed kernel (four records per wave): 2.0-2.4x
-// faster than the small shape for records of 64 B - 2 KiB, 3 % slower at
-// 4 KiB (profiles/r3/ab_packed_sizes.jsonl)
-[[maybe_unused]] constexpr uint64_t TINY_RECORD_MAX = 2048;
-// ... in rows of 8 lanes (eight records per wave) up to 1 KiB and of 4 lanes
-// (sixteen per wave) up to 256 B: every packet then takes one superstep, and
-// more records share its per-packet work (Zipf <= 1 KiB -8 %, Zipf <= 512 B
-// -31 %, Zipf <= 256 B -55 %, 64 B records -71 % against rows of 16;
-// profiles/r3/ab_packed_row_width*.jsonl)
-[[maybe_unused]] constexpr uint64_t TINY8_RECORD_MAX = 1024;
-[[maybe_unused]] constexpr uint64_t TINY4_RECORD_MAX = 256;
+[[maybe_unused]] constexpr uint64_t TINY_RECORD_MAX = 4096;
+[[maybe_unused]] constexpr uint64_t TINY8_RECORD_MAX = 2048;
+[[maybe_unused]] constexpr uint64_t TINY4_RECORD_MAX = 512;
 // record-relative grids of records this long load from the dword below the
 // record and fold its last bytes in at the end (next_seg_batched): the fold
 // waits for one dword load at the record's end, which small records cannot
@@ -1050,7 +1048,7 @@ template <int RW>
 struct PkRow {
     static constexpr uint32_t NR = 64 / RW;
     static constexpr uint32_t PPS = K * RW;
-    static_assert(RW == 4 || RW == 8 || RW == 16, "row width");
+    static_assert(RW == 4 || RW == 8 || RW == 16 || RW == 32, "row width");
 };
 
 // one row's record in the current packet (uniform within the row)
@@ -1146,6 +1144,10 @@ __device__ __forceinline__ uint32_t max4rows(uint32_t v) {
 // row rotations fold the rows of a 16-lane DPP row, then four readlanes
 template <int RW>
 __device__ __forceinline__ uint32_t max_rows(uint32_t v) {
+    if constexpr (RW == 32) {
+        const uint32_t a = __builtin_amdgcn_readlane(v, 0), b = __builtin_amdgcn_readlane(v, 32);
+        return a > b ? a : b;
+    }
     if constexpr (RW <= 4) {
         const uint32_t t = __builtin_amdgcn_update_dpp(0u, v, 0x124, 0xF, 0xF, false); // row_ror:4
         v = t > v ? t : v;
@@ -1305,8 +1307,9 @@ __device__ __forceinline__ uint32_t pk_finish(const PkGeo &g, const PkPacket &p,
                                               const uint32_t *lds) {
     // LP column 16 - RW + (lane mod RW) holds the shift by 16 (RW - 1 - lane mod RW)
     // (rows of 16: column lane & 31, one bank per lane; narrower rows share
-    // columns -- a 4-way conflict for rows of 4, once per packet)
-    const uint32_t col = RW == 16 ? (lane & 31u) : (16u - RW) + (lane % RW) + (lane & 16u);
+    // columns -- a 4-way conflict for rows of 4, once per packet); rows of 32
+    // have LT in LP's place, column lane & 31
+    const uint32_t col = RW >= 16 ? (lane & 31u) : (16u - RW) + (lane % RW) + (lane & 16u);
     uint32_t x = 0;
 #pragma unroll
     for (int c = 0; c < SCH; c++)
@@ -1315,10 +1318,12 @@ __device__ __forceinline__ uint32_t pk_finish(const PkGeo &g, const PkPacket &p,
     x ^= __builtin_amdgcn_update_dpp(0u, x, 0x4E, 0xF, 0xF, false);  // quad_perm [2,3,0,1]
     if constexpr (RW == 8)
         x ^= __builtin_amdgcn_update_dpp(0u, x, 0x141, 0xF, 0xF, false); // row_half_mirror
-    if constexpr (RW == 16) {
+    if constexpr (RW >= 16) {
         x ^= __builtin_amdgcn_update_dpp(0u, x, 0x124, 0xF, 0xF, false); // row_ror:4
         x ^= __builtin_amdgcn_update_dpp(0u, x, 0x128, 0xF, 0xF, false); // row_ror:8
     }
+    if constexpr (RW == 32) // the two 16-lane halves of a row
+        x ^= __shfl_xor(x, 16, 64);
     if (p.anyh) { // F[0] is the identity: rows without fold bytes pass through
         const uint32_t h = (g.fl >> 4) & 3u;
         const uint32_t y = VM ? g.y : row_pick(lane, p.y[0], p.y[1], p.y[2], p.y[3]);
@@ -1369,7 +1374,7 @@ __device__ __forceinline__ uint64_t pk_first_record(const UnitPrefix &us, uint64
 // have landed (one superstep of loads in flight per wave); 0 = two
 
 template <int WGT, int WPE, int DYN = 4, int CPW = 4, uint32_t DYN_POOLS = 32, bool SP = true, int WAITP = 0,
-          bool NTL = true, bool VM = false, int RW = 16>
+          bool NTL = true, bool VM = false, int RW = 16, bool SB = false>
 __global__ __launch_bounds__(WGT, WPE) void crc_packed_kernel(
     const uint8_t *__restrict__ arena, const uint64_t *__restrict__ offsets,
     const uint32_t *__restrict__ lengths, const PlanArgs plan, uint64_t n,
@@ -1437,8 +1442,11 @@ __global__ __launch_bounds__(WGT, WPE) void crc_packed_kernel(
     {
         // the LDS image [F | TP | WP | LP]; narrower rows take their slot and
         // advance tables from TE/WE or TQ/WQ
-        constexpr uint32_t TSRC = RW == 16 ? ZDBCRC_OFF_TP : RW == 8 ? ZDBCRC_OFF_TE : ZDBCRC_OFF_TQ;
-        constexpr uint32_t WSRC = RW == 16 ? ZDBCRC_OFF_WP : RW == 8 ? ZDBCRC_OFF_WE : ZDBCRC_OFF_WQ;
+        constexpr uint32_t TSRC = RW == 32 ? ZDBCRC_OFF_TT : RW == 16 ? ZDBCRC_OFF_TP : RW == 8 ? ZDBCRC_OFF_TE
+                                                                                              : ZDBCRC_OFF_TQ;
+        constexpr uint32_t WSRC = RW == 32 ? ZDBCRC_OFF_WT : RW == 16 ? ZDBCRC_OFF_WP : RW == 8 ? ZDBCRC_OFF_WE
+                                                                                              : ZDBCRC_OFF_WQ;
+        constexpr uint32_t LSRC = RW == 32 ? ZDBCRC_OFF_LT : ZDBCRC_OFF_LP;
         static_assert(TSRC % 4 == 0 && WSRC % 4 == 0 && PK_TP % 4 == 0 && PK_WP % 4 == 0 && PK_LP % 4 == 0,
                       "16-byte granular table ranges");
         const uint4 *src = reinterpret_cast<const uint4 *>(tables);
@@ -1448,7 +1456,7 @@ __global__ __launch_bounds__(WGT, WPE) void crc_packed_kernel(
             const uint32_t sdw = d < PK_TP ? ZDBCRC_OFF_F + d
                                  : d < PK_WP ? TSRC + (d - PK_TP)
                                  : d < PK_LP ? WSRC + (d - PK_WP)
-                                             : ZDBCRC_OFF_F + d;
+                                             : LSRC + (d - PK_LP);
             dst[i] = src[sdw / 4];
         }
     }
@@ -1516,6 +1524,44 @@ __global__ __launch_bounds__(WGT, WPE) void crc_packed_kernel(
         };
         issue(gc, pc, 0, cur);
         uint32_t css = 0, acc = 0;
+        if constexpr (SB) {
+            // one load buffer: a wave folds a superstep, then issues the
+            // next one's loads (the other waves of its SIMD cover the wait);
+            // 16 + 5 VGPRs fewer than the double-buffered loop below
+            for (;;) {
+                const bool newp = css + 1 == pc.S;
+                const bool last = newp && pc.r0 + NR >= rb;
+                if ((int32_t)(R::PPS * css) > pc.kmax)
+                    acc = pk_superstep<false, false, RW>(gc, pc, acc, cur, css, lane, lds);
+                else if (pc.anyd)
+                    acc = pk_superstep<true, true, RW>(gc, pc, acc, cur, css, lane, lds);
+                else
+                    acc = pk_superstep<true, false, RW>(gc, pc, acc, cur, css, lane, lds);
+                uint32_t *dst = dwave;
+                uint32_t x = 0;
+                if (newp) {
+                    x = pk_finish<VM, RW>(gc, pc, acc, lane, lds);
+                    acc = 0;
+                    if (lane / RW < pc.nr && !(gc.fl & PK_NOSTORE))
+                        dst = out + pc.r0 + lane / RW;
+                }
+                if (lane % RW == 0)
+                    *dst = x;
+                if (last)
+                    break;
+                if (newp) {
+                    const uint64_t rn = pc.r0 + NR;
+                    pk_geometry<VM, RW>(pk_addr<VM>(m, ab, lane), pk_len<VM>(m, lane), rn, rb, lane, dummy,
+                                        plan.cls_max, gc, pc);
+                    css = 0;
+                } else {
+                    css++;
+                }
+                issue(gc, pc, css, cur);
+            }
+            r0 = rb;
+            continue;
+        }
         for (;;) {
             const bool newp = css + 1 == pc.S;
             const bool last = newp && pc.r0 + NR >= rb; // the range ends with this packet
@@ -1575,17 +1621,20 @@ struct KernelVariant {
     uint32_t unit_ovh = UNIT_OVH; // must match the kernel's UO
 };
 
-// batches of records <= 2 KiB: the packed kernel (512 threads: the 768-thread
-// build spills, profiles/r3/ab_packed_kernel.jsonl) with vector-loaded
-// descriptors and fold dwords and one superstep of loads in flight
-// (fixed 2 KiB -16 %, Zipf <= 2 KiB -13 %, 256 B records -23 % against the
-// scalar-loaded first version, profiles/r3/ab_packed_vm*.jsonl)
-const KernelVariant kTiny = {"pk_wg512_dyn4c4p32_sp_wait_vm", crc_packed_kernel<512, 4, 4, 4, 32, true, 1, true, true>,
-                             512, WG_PER_CU, UO_PK};
-const KernelVariant kTiny8 = {"pk8_wg512_dyn4c4p32_sp_wait_vm",
-                              crc_packed_kernel<512, 4, 4, 4, 32, true, 1, true, true, 8>, 512, WG_PER_CU, UO_PK};
-const KernelVariant kTiny4 = {"pk4_wg512_dyn4c4p32_sp_wait_vm",
-                              crc_packed_kernel<512, 4, 4, 4, 32, true, 1, true, true, 4>, 512, WG_PER_CU, UO_PK};
+// batches of records <= 4 KiB: the packed kernel with vector-loaded
+// descriptors and fold dwords and ONE load buffer -- a wave
+// folds a superstep, then issues the next one's loads; the other waves of its
+// SIMD cover the wait -- which brings it to 74 VGPRs, i.e. 768 threads and 6
+// waves per SIMD (the double-buffered 512-thread form ran 4): fixed 4 KiB
+// 0.798 -> 0.709 ms, Zipf <= 2 KiB 2.70 -> 2.31 (profiles/r3/ab_packed_single_buffer.jsonl)
+const KernelVariant kTiny = {"pk_wg768_dyn4c4p32_sp_vm_sb",
+                             crc_packed_kernel<768, 6, 4, 4, 32, true, 0, true, true, 16, true>, 768, WG_PER_CU,
+                             UO_PK};
+const KernelVariant kTiny8 = {"pk8_wg768_dyn4c4p32_sp_vm_sb",
+                              crc_packed_kernel<768, 6, 4, 4, 32, true, 0, true, true, 8, true>, 768, WG_PER_CU, UO_PK};
+const KernelVariant kTiny4 = {"pk4_wg768_dyn4c4p32_sp_vm_sb",
+                              crc_packed_kernel<768, 6, 4, 4, 32, true, 0, true, true, 4, true>, 768, WG_PER_CU, UO_PK};
+
 // Diagnostic library only (A/B): a batch without a known bound split by
 // record size -- records of at most `split` bytes to the packed kernel, the
 // rest to the main kernel, planned in one planner launch (two unit prefixes,
@@ -1676,6 +1725,13 @@ const KernelVariant kVariants[] = {
     {"pk4_wg512_dyn4c4p32_sp_wait_vm", crc_packed_kernel<512, 4, 4, 4, 32, true, 1, true, true, 4>, 512, WG_PER_CU, UO_PK},
     {"pk8_wg512_dyn4c4p32_sp_vm", crc_packed_kernel<512, 4, 4, 4, 32, true, 0, true, true, 8>, 512, WG_PER_CU, UO_PK},
     {"pk4_wg512_dyn4c4p32_sp_vm", crc_packed_kernel<512, 4, 4, 4, 32, true, 0, true, true, 4>, 512, WG_PER_CU, UO_PK},
+    // single load buffer (fold, then issue the next loads): fits 6 waves per SIMD
+    {"pk_wg768_dyn4c4p32_sp_vm_sb", crc_packed_kernel<768, 6, 4, 4, 32, true, 0, true, true, 16, true>, 768, WG_PER_CU, UO_PK},
+    {"pk8_wg768_dyn4c4p32_sp_vm_sb", crc_packed_kernel<768, 6, 4, 4, 32, true, 0, true, true, 8, true>, 768, WG_PER_CU, UO_PK},
+    {"pk_wg512_dyn4c4p32_sp_vm_sb", crc_packed_kernel<512, 4, 4, 4, 32, true, 0, true, true, 16, true>, 512, WG_PER_CU, UO_PK},
+    {"pk4_wg768_dyn4c4p32_sp_vm_sb", crc_packed_kernel<768, 6, 4, 4, 32, true, 0, true, true, 4, true>, 768, WG_PER_CU, UO_PK},
+    // rows of 32 lanes (two records per wave)
+    {"pk32_wg768_dyn4c4p32_sp_vm_sb", crc_packed_kernel<768, 6, 4, 4, 32, true, 0, true, true, 32, true>, 768, WG_PER_CU, UO_PK},
 
 };
 constexpr int kNumVariants = (int)(sizeof(kVariants) / sizeof(kVariants[0]));
@@ -1697,39 +1753,25 @@ const KernelVariant &variant(uint64_t /*max_len: the A/B harness picks by index*
     return kVariants[v];
 }
 #else
-// the product library ships the checksum kernel in two loop shapes, no
-// environment knob: tail pool (4/16 of the units, 32 pools drawn from every
-// XCD, 4 chunks per wave) with static-phase priority, 768 threads,
-// nontemporal payload loads
-// (DESIGN.md §4.1); the small-record shape (PP 3: the loop unrolled twice,
-// load buffers swapping roles instead of 16 register copies per superstep,
-// the next loads issued once the previous ones have landed) for batches
-// whose records are known to be <= 4 KiB -- C2 -3.7 %, C2u -3.9 %, but C3
-// +4 % (profiles/r2/ab_ppw.jsonl); both shapes are exact for any input, the
-// choice only changes speed.  (One kernel holding both loops
-// needs more than the 80 VGPRs six waves per SIMD allow: 40 B/lane of
-// scratch.)
+// the product library ships the main checksum kernel (any records; tail
+// pool: 4/16 of the units, 32 pools drawn from every XCD, 4 chunks per wave,
+// static-phase priority, 768 threads, nontemporal payload loads; DESIGN.md
+// §4.1) and the packed kernel for batches known to hold records of at most
+// 4 KiB (above), no environment knob.  Every shape is exact for any input;
+// the choice only changes speed.
 const KernelVariant kDefault = {"v3_wg768_nt_dyn4c4p32_sp_xp",
                                 crc_batch_kernel_v3<768, 6, false, 0, UNIT_OVH, false, true, false, 0, 4, 4, 32, true,
                                                     0, false, false, true>,
                                 768};
-// (its records are below DWG_MIN_BYTES, so it is built without the dword
-// grid's code: BMG)
-const KernelVariant kSmall = {"v3_wg768_nt_dyn4c4p32_sp_pp_wait_bmg_xp",
-                              crc_batch_kernel_v3<768, 6, false, 0, UNIT_OVH, false, true, false, 0, 4, 4, 32, true, 3,
-                                                  false, true, true>,
-                              768};
 // the product never splits a batch (diagnostic A/B only)
 constexpr uint32_t split_bytes(const KernelVariant &) { return 0u; }
 // the kernel for a batch whose records are at most max_len bytes (0: unknown)
 const KernelVariant &variant(uint64_t max_len = 0) {
-    if (max_len == 0 || max_len > SMALL_RECORD_MAX)
+    if (max_len == 0 || max_len > TINY_RECORD_MAX)
         return kDefault;
     if (max_len <= TINY4_RECORD_MAX)
         return kTiny4;
-    if (max_len <= TINY8_RECORD_MAX)
-        return kTiny8;
-    return max_len <= TINY_RECORD_MAX ? kTiny : kSmall;
+    return max_len <= TINY8_RECORD_MAX ? kTiny8 : kTiny;
 }
 #endif
 

@@ -214,11 +214,11 @@ void zdbcrc_build_tables(uint32_t *img) {
             b[t] = multmodp(mwp, reg_slice(1u << t, c));
         fill_linear(img + ZDBCRC_OFF_WP + c * 32, 1, b);
     }
-    /* narrower rows: 8 lanes (128 B per slot), 4 lanes (64 B per slot) */
-    for (int nr = 0; nr < 2; nr++) {
-        const uint64_t slot = nr ? 64 : 128;
-        uint32_t *const tt = img + (nr ? ZDBCRC_OFF_TQ : ZDBCRC_OFF_TE);
-        uint32_t *const tw = img + (nr ? ZDBCRC_OFF_WQ : ZDBCRC_OFF_WE);
+    /* other row widths: 8 lanes (128 B per slot), 4 lanes (64 B), 32 lanes (512 B) */
+    for (int nr = 0; nr < 3; nr++) {
+        const uint64_t slot = nr == 0 ? 128 : nr == 1 ? 64 : 512;
+        uint32_t *const tt = img + (nr == 0 ? ZDBCRC_OFF_TE : nr == 1 ? ZDBCRC_OFF_TQ : ZDBCRC_OFF_TT);
+        uint32_t *const tw = img + (nr == 0 ? ZDBCRC_OFF_WE : nr == 1 ? ZDBCRC_OFF_WQ : ZDBCRC_OFF_WT);
         for (int i = 0; i < ZDBCRC_K; i++) {
             const uint32_t m = xpow(8 * slot * (uint64_t)(ZDBCRC_K - 1 - i), 0);
             for (int c = 0; c < ZDBCRC_PCH; c++) {
@@ -240,6 +240,14 @@ void zdbcrc_build_tables(uint32_t *img) {
             for (int t = 0; t < 5; t++)
                 b[t] = multmodp(m, reg_slice(1u << t, c));
             fill_linear(img + ZDBCRC_OFF_LP + c * 32 * 32 + l, 32, b);
+        }
+    }
+    for (int l = 0; l < 32; l++) {
+        const uint32_t m = xpow(8 * 16 * (uint64_t)(31 - l), 0);
+        for (int c = 0; c < ZDBCRC_SCH; c++) {
+            for (int t = 0; t < 5; t++)
+                b[t] = multmodp(m, reg_slice(1u << t, c));
+            fill_linear(img + ZDBCRC_OFF_LT + c * 32 * 32 + l, 32, b);
         }
     }
 }

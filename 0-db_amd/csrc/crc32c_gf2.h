@@ -64,7 +64,11 @@ uint32_t zdbcrc_update_bytes(uint32_t crc, const uint8_t *p, size_t n);
 #define ZDBCRC_OFF_WE   (ZDBCRC_OFF_TE + ZDBCRC_K * ZDBCRC_PCH * 32)        /* [SCH][32]            */
 #define ZDBCRC_OFF_TQ   (ZDBCRC_OFF_WE + ZDBCRC_SCH * 32)                   /* [K][PCH][32] rows of 4 */
 #define ZDBCRC_OFF_WQ   (ZDBCRC_OFF_TQ + ZDBCRC_K * ZDBCRC_PCH * 32)        /* [SCH][32]            */
-#define ZDBCRC_TABLE_DW (ZDBCRC_OFF_WQ + ZDBCRC_SCH * 32)
+/* rows of 32 lanes (two records per wave): slot, advance and placement tables */
+#define ZDBCRC_OFF_TT   (ZDBCRC_OFF_WQ + ZDBCRC_SCH * 32)                   /* [K][PCH][32]         */
+#define ZDBCRC_OFF_WT   (ZDBCRC_OFF_TT + ZDBCRC_K * ZDBCRC_PCH * 32)        /* [SCH][32]            */
+#define ZDBCRC_OFF_LT   (ZDBCRC_OFF_WT + ZDBCRC_SCH * 32)                   /* [SCH][32][32]        */
+#define ZDBCRC_TABLE_DW (ZDBCRC_OFF_LT + ZDBCRC_SCH * 32 * 32)
 
 /*
  * Piece windows.  A 16-byte piece (dwords w0..w3, little endian) is covered
@@ -107,6 +111,8 @@ int zdbcrc_window_bit(int j, int t);
  * TE, TQ[i][j][v]: as T, shifted by 16 RW (K-1-i) bytes
  * WE, WQ[c][v]   : shift(v << 5c, 64 RW)
  * (placement by 16 (RW-1-l) bytes reads LP's column 16 - RW + l)
+ * Rows of 32 lanes: TT (512 B per slot), WT (2 KiB), and
+ * LT[c][v][l]    : shift(v << 5c, 16*(31-l)), l = lane & 31
  */
 void zdbcrc_build_tables(uint32_t *image /* ZDBCRC_TABLE_DW dwords */);
 

@@ -874,7 +874,7 @@ def main():
             do2, dl2 = torch.from_numpy(o2).cuda(), torch.from_numpy(l2.astype(np.int32)).cuda()
             out2 = torch.empty(len(l2), dtype=torch.int32, device="cuda")
             # C2 / C2u: fixed 4 KiB values -- the caller knows the bound
-            # (zdb_crc32_batch_device_sized picks the small-record shape)
+            # (zdb_crc32_batch_device_sized picks the packed kernel, rows of 16 lanes)
             ml = 4096 if other in ("fixed4k", "c2u") else None
             t_settle = time.perf_counter() + args.settle_s / 2
             while time.perf_counter() < t_settle:
@@ -895,7 +895,7 @@ def main():
             p2 = workload_parity(other, out2, 0, args.gib)
             log(f"{other} parity: {p2}")
             extra[other] = {"desc": d2, "records": len(l2), "gibs": round(pb * args.steps / (tb - ta) / GIB, 2),
-                            "shape": "small-record (max_length 4096)" if ml else "default",
+                            "shape": "packed kernel, rows of 16 lanes (max_length 4096)" if ml else "default",
                             "parity": p2, "kernel_ms": round(km / max(kl, 1), 4),
                             "roofline_frac": round((pb + 16 * len(l2)) / (km / max(kl, 1) / 1e3) / 1e9
                                                    / HBM_PEAK_GBS, 4)}

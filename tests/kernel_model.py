@@ -26,8 +26,11 @@ OFF_TE = OFF_LP + SCH * 32 * 32  # rows of 8 lanes: slot tables (128 B per slot)
 OFF_WE = OFF_TE + K * PCH * 32   # ... advance over 512 B
 OFF_TQ = OFF_WE + SCH * 32       # rows of 4 lanes: slot tables (64 B per slot)
 OFF_WQ = OFF_TQ + K * PCH * 32   # ... advance over 256 B
-TABLE_DW = OFF_WQ + SCH * 32
-PK_TABLES = {16: (OFF_TP, OFF_WP), 8: (OFF_TE, OFF_WE), 4: (OFF_TQ, OFF_WQ)}
+OFF_TT = OFF_WQ + SCH * 32       # rows of 32 lanes: slot tables (512 B per slot)
+OFF_WT = OFF_TT + K * PCH * 32   # ... advance over 2 KiB
+OFF_LT = OFF_WT + SCH * 32       # ... placement of lane l & 31 in its row of 32
+TABLE_DW = OFF_LT + SCH * 32 * 32
+PK_TABLES = {32: (OFF_TT, OFF_WT), 16: (OFF_TP, OFF_WP), 8: (OFF_TE, OFF_WE), 4: (OFF_TQ, OFF_WQ)}
 UNIT_OVH = 384
 DWG_MIN_BYTES = 64 * 1024  # record-relative grids this long load from the dword below the record
 MIN_UNITS_PER_WAVE = 256
@@ -286,9 +289,10 @@ def packed_row_crc(mem: np.ndarray, mem_base: int, A: int, L: int, S: int, row: 
             acc ^= np.bitwise_xor.reduce(tab[idx], axis=1).astype(np.uint32)
     sl = _slices32(acc)
     lanes = rw * row + np.arange(rw, dtype=np.int64)
-    # LP column of lane l: l & 31 for rows of 16, else 16 - rw + l mod rw (+16 in the upper half)
-    col = lanes & 31 if rw == 16 else (16 - rw) + lanes % rw + (lanes & 16)
-    idx = OFF_LP + (np.arange(SCH)[None, :] * 32 + sl) * 32 + col[:, None]
+    # LP column of lane l: l & 31 for rows of 16, else 16 - rw + l mod rw (+16 in the upper half);
+    # rows of 32 read LT at column l & 31
+    col = lanes & 31 if rw >= 16 else (16 - rw) + lanes % rw + (lanes & 16)
+    idx = (OFF_LT if rw == 32 else OFF_LP) + (np.arange(SCH)[None, :] * 32 + sl) * 32 + col[:, None]
     x = int(np.bitwise_xor.reduce(np.bitwise_xor.reduce(tab[idx], axis=1)))
     if g["h"]:
         y = int.from_bytes(mem[g["Ep"] - mem_base:g["E"] - mem_base].tobytes(), "little")

@@ -244,9 +244,9 @@ def test_full_size_c2_digest(dev, oracle_c, digests):
 def test_full_size_small_record_digests(dev, oracle_c, digests, workload, max_length):
     """C2 (4 KiB-aligned) and C2u (4 KiB payloads behind 26-byte datafile
     headers, byte-misaligned: SURVEY §8(d)) at full size, 1 Mi records each,
-    in BOTH loop shapes the library carries -- the default and the
-    small-record shape that zdb_crc32_batch_device_sized picks for
-    max_length <= 4096, i.e. the shape bench.py times for these workloads --
+    in BOTH kernels the library carries for them -- the main kernel and the
+    packed kernel (rows of 16 lanes) that zdb_crc32_batch_device_sized picks
+    for max_length <= 4096, i.e. the shape bench.py times for these workloads --
     bit-exact vs the reference's digest (make_golden.py --only-c2u)."""
     sys.path.insert(0, str(ROOT))
     import bench
@@ -265,7 +265,7 @@ def test_full_size_small_record_digests(dev, oracle_c, digests, workload, max_le
     del arena
 
 
-@pytest.mark.parametrize("bound", [256, 1024, 2048])
+@pytest.mark.parametrize("bound", [512, 2048, 4096])
 def test_packed_shapes_at_scale(dev, oracle_c, bound):
     """each packed shape (rows of 4 / 8 / 16 lanes) on 512 MiB of C3's own
     record sizes up to its bound (Zipf, tiled; records at every alignment):
@@ -652,9 +652,9 @@ def test_batched_check_empty_payload_key_past_end(dev, oracle_c, integrity, want
 
 @pytest.mark.parametrize("case", ["fixed4k", "fixed4k_misaligned", "small_mixed", "hint_too_small"])
 def test_small_record_shape(dev, oracle_c, case):
-    """zdb_crc32_batch_device_sized: the small-record loop shape (records <=
-    4 KiB known to the caller) is bit-exact -- also when the caller's bound is
-    wrong (a 300 KiB record under a 4 KiB hint only costs speed)"""
+    """zdb_crc32_batch_device_sized with a 4 KiB bound (the packed kernel in
+    rows of 16 lanes) is bit-exact -- also when the caller's bound is wrong
+    (a 300 KiB record under a 4 KiB hint only costs speed)"""
     rng = np.random.default_rng(7)
     if case.startswith("fixed4k"):
         n = 3000
@@ -684,9 +684,9 @@ def test_small_record_shape(dev, oracle_c, case):
 
 
 def _packed_cases():
-    """crafted batches for the packed kernel (records <= 2 KiB: four per wave,
-    one per row of 16 lanes; dword-anchored grid, piece 0 shifted up when a
-    record starts in the first 16 bytes of a page)"""
+    """crafted batches for the packed kernel (records <= 4 KiB: one per row
+    of 4 / 8 / 16 lanes by the bound; dword-anchored grid, piece 0 shifted up
+    when a record starts in the first 16 bytes of a page)"""
     rng = np.random.default_rng(5)
     out = {}
     lens = np.arange(0, 301)
@@ -711,8 +711,8 @@ def _packed_cases():
     out["hint_too_small"] = (offs, lens, 2048)  # the bound is wrong: still exact
     lens = np.full(1 << 16, 64)
     out["fixed_64B"] = (np.arange(1 << 16, dtype=np.int64) * 64, lens, 64)
-    # narrower rows: bounds <= 256 B take rows of 4 lanes, <= 1 KiB rows of 8
-    for bound in (256, 1024):
+    # row widths by bound: <= 512 B rows of 4 lanes, <= 2 KiB rows of 8, <= 4 KiB rows of 16
+    for bound in (256, 1024, 4096):
         lens = rng.integers(0, bound + 1, 100_000)
         offs = np.zeros(len(lens), np.int64)
         offs[1:] = np.cumsum(lens[:-1] + rng.integers(0, 5, len(lens) - 1))
@@ -755,7 +755,7 @@ def test_packed_kernel_small_records(dev, oracle_c, case):
         dev.batch_device(a, o, l, out, max_length=bound)
         torch.cuda.synchronize()
         np.testing.assert_array_equal(out.cpu().numpy().view(np.uint32), want)
-    if lens.max() <= 2048:  # the host entry takes the packed kernel (its row width) from the lengths themselves
+    if lens.max() <= 4096:  # the host entry takes the packed kernel (its row width) from the lengths themselves
         np.testing.assert_array_equal(dev.batch_host(arena, offs.astype(np.uint64), lens.astype(np.uint32)), want)
 
 

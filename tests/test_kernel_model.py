@@ -139,7 +139,7 @@ def test_tail_pool_guard():
     assert len(km.ranges(10 ** 7, 16, 64 * chunk + 1, 16, dyn=6, pools=8)) == 16
 
 
-@pytest.mark.parametrize("rw", [16, 8, 4])
+@pytest.mark.parametrize("rw", [32, 16, 8, 4])
 @pytest.mark.parametrize("force_shifted_first", [False, True])
 @pytest.mark.parametrize("base", [0, 1, 2, 3, 13])
 def test_packed_small_records(oracle_c, tab, base, force_shifted_first, rw):
@@ -160,7 +160,7 @@ def test_packed_small_records(oracle_c, tab, base, force_shifted_first, rw):
     np.testing.assert_array_equal(got, oracle_c.batch(arena, offs, lens))
 
 
-@pytest.mark.parametrize("rw", [16, 8, 4])
+@pytest.mark.parametrize("rw", [32, 16, 8, 4])
 def test_packed_long_record_in_packet(oracle_c, tab, rw):
     """a record longer than 4 KiB (a wrong max_length hint) stretches its packet: still exact"""
     lens = np.array([5, 70_000, 4096, 0, 33, 9000])
@@ -169,7 +169,7 @@ def test_packed_long_record_in_packet(oracle_c, tab, rw):
     np.testing.assert_array_equal(km.packed_batch(arena, offs, lens, tab, rw=rw), oracle_c.batch(arena, offs, lens))
 
 
-@pytest.mark.parametrize("rw", [16, 4])
+@pytest.mark.parametrize("rw", [32, 16, 4])
 def test_packed_loads_stay_in_bounds(oracle_c, tab, rw):
     """every load the packed kernel issues (empty positions included) stays in
     A's 4 KiB page from A's 16-byte block on and below the 16-byte boundary
