@@ -666,7 +666,7 @@ __device__ __forceinline__ uint64_t block_excl_scan64(uint64_t v, uint64_t *wsum
 template <int WGT, int WPE, bool STAMP = false, int PRIO = 0, uint32_t UO = UNIT_OVH, int NOZ = 0,
           bool NTL = false, bool NOLOAD = false, int XM = 0, int DYN = 0, int CPW = 4, uint32_t DYN_POOLS = 8,
           bool SP = false, int PP = 0, bool SEGDUMP = false, bool BMG = false, bool XP = false,
-          uint64_t DWGM = DWG_MIN_BYTES, bool FRB = false>
+          uint64_t DWGM = DWG_MIN_BYTES, bool FRB = false, bool SB1 = false>
 __global__ __launch_bounds__(WGT, WPE) void crc_batch_kernel_v3(
     const uint8_t *__restrict__ arena, const uint64_t *__restrict__ offsets,
     const uint32_t *__restrict__ lengths, const PlanArgs plan, uint64_t n,
@@ -896,7 +896,8 @@ __global__ __launch_bounds__(WGT, WPE) void crc_batch_kernel_v3(
         }                                                                                                     \
         if (PP == 3)                                                                                          \
             __builtin_amdgcn_s_waitcnt(0x0F70);                                                               \
-        load_superstep_v3<NTL, NOLOAD>(nx.c, nss, lane, BUFN);                                                \
+        if (!SB1)                                                                                             \
+            load_superstep_v3<NTL, NOLOAD>(nx.c, nss, lane, BUFN);                                            \
         if (css == 0 || css + 1 == cur.S)                                                                     \
             acc = superstep<true, XM>(cur.c, acc, BUFC, css, cur.t0, lane, lds);                              \
         else                                                                                                  \
@@ -922,7 +923,9 @@ __global__ __launch_bounds__(WGT, WPE) void crc_batch_kernel_v3(
             }                                                                                                 \
         }                                                                                                     \
         if (lane == 0)                                                                                        \
-            *dst = x;
+            *dst = x;                                                                                         \
+        if (SB1 && more) /* one load buffer: the next superstep's loads after the fold */                    \
+            load_superstep_v3<NTL, NOLOAD>(nx.c, nss, lane, BUFC);
 
     if (PP && pp) { // ping-pong: the two load buffers swap roles, no register copies
         for (;;) {
@@ -948,9 +951,11 @@ __global__ __launch_bounds__(WGT, WPE) void crc_batch_kernel_v3(
                 break;
             cur = nx;
             css = nss;
+            if (!SB1) {
 #pragma unroll
-            for (int i = 0; i < K; i++)
-                bufc[i] = bufn[i];
+                for (int i = 0; i < K; i++)
+                    bufc[i] = bufn[i];
+            }
         }
     }
 #undef ZDBCRC_STEP
@@ -1730,6 +1735,9 @@ const KernelVariant kVariants[] = {
     {"pk8_wg768_dyn4c4p32_sp_vm_sb", crc_packed_kernel<768, 6, 4, 4, 32, true, 0, true, true, 8, true>, 768, WG_PER_CU, UO_PK},
     {"pk_wg512_dyn4c4p32_sp_vm_sb", crc_packed_kernel<512, 4, 4, 4, 32, true, 0, true, true, 16, true>, 512, WG_PER_CU, UO_PK},
     {"pk4_wg768_dyn4c4p32_sp_vm_sb", crc_packed_kernel<768, 6, 4, 4, 32, true, 0, true, true, 4, true>, 768, WG_PER_CU, UO_PK},
+    // round 3 (resumed): one load buffer (the next superstep's loads after the fold), more waves per SIMD
+    {"v3_wg1024_nt_dyn4c4p32_sp_xp_sb", crc_batch_kernel_v3<1024, 8, false, 0, UNIT_OVH, false, true, false, 0, 4, 4, 32, true, 0, false, false, true, DWG_MIN_BYTES, false, true>, 1024},
+    {"v3_wg768_nt_dyn4c4p32_sp_xp_sb", crc_batch_kernel_v3<768, 6, false, 0, UNIT_OVH, false, true, false, 0, 4, 4, 32, true, 0, false, false, true, DWG_MIN_BYTES, false, true>, 768},
     // rows of 32 lanes (two records per wave)
     {"pk32_wg768_dyn4c4p32_sp_vm_sb", crc_packed_kernel<768, 6, 4, 4, 32, true, 0, true, true, 32, true>, 768, WG_PER_CU, UO_PK},
 
