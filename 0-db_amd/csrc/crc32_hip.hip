@@ -1629,16 +1629,20 @@ struct KernelVariant {
 // batches of records <= 4 KiB: the packed kernel with vector-loaded
 // descriptors and fold dwords and ONE load buffer -- a wave
 // folds a superstep, then issues the next one's loads; the other waves of its
-// SIMD cover the wait -- which brings it to 74 VGPRs, i.e. 768 threads and 6
-// waves per SIMD (the double-buffered 512-thread form ran 4): fixed 4 KiB
-// 0.798 -> 0.709 ms, Zipf <= 2 KiB 2.70 -> 2.31 (profiles/r3/ab_packed_single_buffer.jsonl)
-const KernelVariant kTiny = {"pk_wg768_dyn4c4p32_sp_vm_sb",
-                             crc_packed_kernel<768, 6, 4, 4, 32, true, 0, true, true, 16, true>, 768, WG_PER_CU,
+// SIMD cover the wait.  That brought it to 74 VGPRs and 768 threads (6 waves
+// per SIMD; the double-buffered 512-thread form ran 4): fixed 4 KiB 0.798 ->
+// 0.709 ms, Zipf <= 2 KiB 2.70 -> 2.31 (profiles/r3/ab_packed_single_buffer.jsonl).
+// Squeezed to 64 VGPRs for 1024 threads (8 waves per SIMD) it gains another
+// 1-8 % on every shape and bound measured (profiles/r3/ab_packed_8waves*.jsonl).
+const KernelVariant kTiny = {"pk_wg1024_dyn4c4p32_sp_vm_sb",
+                             crc_packed_kernel<1024, 8, 4, 4, 32, true, 0, true, true, 16, true>, 1024, WG_PER_CU,
                              UO_PK};
-const KernelVariant kTiny8 = {"pk8_wg768_dyn4c4p32_sp_vm_sb",
-                              crc_packed_kernel<768, 6, 4, 4, 32, true, 0, true, true, 8, true>, 768, WG_PER_CU, UO_PK};
-const KernelVariant kTiny4 = {"pk4_wg768_dyn4c4p32_sp_vm_sb",
-                              crc_packed_kernel<768, 6, 4, 4, 32, true, 0, true, true, 4, true>, 768, WG_PER_CU, UO_PK};
+const KernelVariant kTiny8 = {"pk8_wg1024_dyn4c4p32_sp_vm_sb",
+                              crc_packed_kernel<1024, 8, 4, 4, 32, true, 0, true, true, 8, true>, 1024, WG_PER_CU,
+                              UO_PK};
+const KernelVariant kTiny4 = {"pk4_wg1024_dyn4c4p32_sp_vm_sb",
+                              crc_packed_kernel<1024, 8, 4, 4, 32, true, 0, true, true, 4, true>, 1024, WG_PER_CU,
+                              UO_PK};
 
 // Diagnostic library only (A/B): a batch without a known bound split by
 // record size -- records of at most `split` bytes to the packed kernel, the
@@ -1738,6 +1742,13 @@ const KernelVariant kVariants[] = {
     // round 3 (resumed): one load buffer (the next superstep's loads after the fold), more waves per SIMD
     {"v3_wg1024_nt_dyn4c4p32_sp_xp_sb", crc_batch_kernel_v3<1024, 8, false, 0, UNIT_OVH, false, true, false, 0, 4, 4, 32, true, 0, false, false, true, DWG_MIN_BYTES, false, true>, 1024},
     {"v3_wg768_nt_dyn4c4p32_sp_xp_sb", crc_batch_kernel_v3<768, 6, false, 0, UNIT_OVH, false, true, false, 0, 4, 4, 32, true, 0, false, false, true, DWG_MIN_BYTES, false, true>, 768},
+    // one-buffer packed kernel with plain (temporal) payload loads: a row's segments share lines at their edges
+    {"pk_wg768_dyn4c4p32_sp_vm_sb_tl", crc_packed_kernel<768, 6, 4, 4, 32, true, 0, false, true, 16, true>, 768, WG_PER_CU, UO_PK},
+    {"pk8_wg768_dyn4c4p32_sp_vm_sb_tl", crc_packed_kernel<768, 6, 4, 4, 32, true, 0, false, true, 8, true>, 768, WG_PER_CU, UO_PK},
+    // one-buffer packed kernel at 8 waves per SIMD (1024-thread workgroups, <= 64 VGPRs)
+    {"pk_wg1024_dyn4c4p32_sp_vm_sb", crc_packed_kernel<1024, 8, 4, 4, 32, true, 0, true, true, 16, true>, 1024, WG_PER_CU, UO_PK},
+    {"pk8_wg1024_dyn4c4p32_sp_vm_sb", crc_packed_kernel<1024, 8, 4, 4, 32, true, 0, true, true, 8, true>, 1024, WG_PER_CU, UO_PK},
+    {"pk4_wg1024_dyn4c4p32_sp_vm_sb", crc_packed_kernel<1024, 8, 4, 4, 32, true, 0, true, true, 4, true>, 1024, WG_PER_CU, UO_PK},
     // rows of 32 lanes (two records per wave)
     {"pk32_wg768_dyn4c4p32_sp_vm_sb", crc_packed_kernel<768, 6, 4, 4, 32, true, 0, true, true, 32, true>, 768, WG_PER_CU, UO_PK},
 

@@ -83,9 +83,9 @@ int zdb_crc32_batch_device(const uint8_t *d_arena, const uint64_t *d_offsets,
 
 /* As zdb_crc32_batch_device, for a caller that knows an upper bound of its
  * record lengths (max_length, 0 = unknown): batches of records <= 4 KiB
- * (fixed-size values, pipelined small SETs) take the small-record loop shape
- * of the kernel, batches of records <= 2 KiB / 1 KiB / 256 B the packed
- * kernel (4 / 8 / 16 records per wave).  Exact for any input; a record longer
+ * (fixed-size values, pipelined small SETs) take the packed kernel, one
+ * record per row of 16 lanes (4 per wave); <= 2 KiB rows of 8 lanes, <= 512 B
+ * rows of 4 (8 / 16 records per wave).  Exact for any input; a record longer
  * than the bound only costs speed.  The host-buffer entry points measure the
  * bound themselves. */
 int zdb_crc32_batch_device_sized(const uint8_t *d_arena, const uint64_t *d_offsets,

@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Summarise rocprofv3 --pmc passes (scripts/profile_pmc.sh) per dispatch of
-crc_batch_kernel: mean counter value over the dispatches, plus the derived
+crc_batch_kernel (or the kernel named by argv[2]): mean counter value over the dispatches, plus the derived
 HBM bytes (FETCH_SIZE x 2 on gfx950 for wide streaming reads, per
 MI355X_MICROARCH.md §HBM) and effective clock."""
 import csv, json, sys
@@ -8,10 +8,11 @@ from collections import defaultdict
 from pathlib import Path
 
 root = Path(sys.argv[1])
+kname = sys.argv[2] if len(sys.argv) > 2 else "crc_batch_kernel"  # e.g. crc_packed_kernel
 vals = defaultdict(lambda: defaultdict(float))
 for f in sorted(root.glob("pass*/pmc_counter_collection.csv")):
     for r in csv.DictReader(open(f)):
-        if "crc_batch_kernel" not in r["Kernel_Name"]:
+        if kname not in r["Kernel_Name"]:
             continue
         vals[r["Counter_Name"]][(f.parent.name, r["Dispatch_Id"])] += float(r["Counter_Value"])
 summary = {k: sum(v.values()) / len(v) for k, v in vals.items()}
