@@ -559,7 +559,9 @@ __device__ __forceinline__ bool next_seg_batched(uint64_t &r, uint64_t n, uint64
 
 // loads of superstep ss: uniform base (segment's first piece) + 32-bit lane
 // offset; lanes before the segment re-read its first piece (zeroed later)
-template <bool NTL = false, bool NOLOAD = false>
+// TEL (with NTL): as pk_load's -- the lanes reaching the line of the
+// superstep's last byte load without the nontemporal hint
+template <bool NTL = false, bool NOLOAD = false, int TEL = 0>
 __device__ __forceinline__ void load_superstep_v3(const SegCtx &s, uint32_t ss, uint32_t lane, uint4 (&buf)[K]) {
     const uint64_t base = s.P0 + 16u * (uint64_t)s.pa;
     const int32_t rel0 = (int32_t)(s.base_j - (int64_t)s.pa) + 64 * (int32_t)(ss * K) + (int32_t)lane;
@@ -573,7 +575,17 @@ __device__ __forceinline__ void load_superstep_v3(const SegCtx &s, uint32_t ss, 
             buf[i] = make_uint4(a, a * 0x9E3779B9u, a ^ 0x5bd1e995u, a + ss);
             continue;
         }
-        const u32x4 v = NTL ? __builtin_nontemporal_load(p) : *p;
+        u32x4 v;
+        if constexpr (NTL && TEL > 0) {
+            const uint64_t a = reinterpret_cast<uint64_t>(p);
+            const uint64_t last = base + ((uint64_t)(uint32_t)(rel0 - (int32_t)lane + 64 * K - 1) << 4) + 15;
+            if (i == K - 1 && ((a + 15) >> 7) == (last >> 7))
+                v = *p;
+            else
+                v = __builtin_nontemporal_load(p);
+        } else {
+            v = NTL ? __builtin_nontemporal_load(p) : *p;
+        }
         buf[i] = make_uint4(v.x, v.y, v.z, v.w);
     }
 }
@@ -666,7 +678,7 @@ __device__ __forceinline__ uint64_t block_excl_scan64(uint64_t v, uint64_t *wsum
 template <int WGT, int WPE, bool STAMP = false, int PRIO = 0, uint32_t UO = UNIT_OVH, int NOZ = 0,
           bool NTL = false, bool NOLOAD = false, int XM = 0, int DYN = 0, int CPW = 4, uint32_t DYN_POOLS = 8,
           bool SP = false, int PP = 0, bool SEGDUMP = false, bool BMG = false, bool XP = false,
-          uint64_t DWGM = DWG_MIN_BYTES, bool FRB = false, bool SB1 = false>
+          uint64_t DWGM = DWG_MIN_BYTES, bool FRB = false, bool SB1 = false, int TEL = 0>
 __global__ __launch_bounds__(WGT, WPE) void crc_batch_kernel_v3(
     const uint8_t *__restrict__ arena, const uint64_t *__restrict__ offsets,
     const uint32_t *__restrict__ lengths, const PlanArgs plan, uint64_t n,
@@ -758,7 +770,7 @@ __global__ __launch_bounds__(WGT, WPE) void crc_batch_kernel_v3(
         load_meta(m, rn, n, lane, unit_start, arena, offsets, lengths);
         active = next_seg_batched<UO, BMG, DWGM>(rn, n, ub, ue, lane, m, unit_start, arena, offsets, lengths, cur);
         if (active)
-            load_superstep_v3<NTL, NOLOAD>(cur.c, 0, lane, bufc);
+            load_superstep_v3<NTL, NOLOAD, TEL>(cur.c, 0, lane, bufc);
     }
     const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     if (PRIO && lane == 0)
@@ -836,7 +848,7 @@ __global__ __launch_bounds__(WGT, WPE) void crc_batch_kernel_v3(
     if (!active) {
         if (!(DYN && dyn && claim(cur)))
             return;
-        load_superstep_v3<NTL, NOLOAD>(cur.c, 0, lane, bufc);
+        load_superstep_v3<NTL, NOLOAD, TEL>(cur.c, 0, lane, bufc);
     }
     const uint32_t young = PRIO >= 2 ? __builtin_amdgcn_readfirstlane(prog[15]) : 0u;
 
@@ -897,7 +909,7 @@ __global__ __launch_bounds__(WGT, WPE) void crc_batch_kernel_v3(
         if (PP == 3)                                                                                          \
             __builtin_amdgcn_s_waitcnt(0x0F70);                                                               \
         if (!SB1)                                                                                             \
-            load_superstep_v3<NTL, NOLOAD>(nx.c, nss, lane, BUFN);                                            \
+            load_superstep_v3<NTL, NOLOAD, TEL>(nx.c, nss, lane, BUFN);                                            \
         if (css == 0 || css + 1 == cur.S)                                                                     \
             acc = superstep<true, XM>(cur.c, acc, BUFC, css, cur.t0, lane, lds);                              \
         else                                                                                                  \
@@ -925,7 +937,7 @@ __global__ __launch_bounds__(WGT, WPE) void crc_batch_kernel_v3(
         if (lane == 0)                                                                                        \
             *dst = x;                                                                                         \
         if (SB1 && more) /* one load buffer: the next superstep's loads after the fold */                    \
-            load_superstep_v3<NTL, NOLOAD>(nx.c, nss, lane, BUFC);
+            load_superstep_v3<NTL, NOLOAD, TEL>(nx.c, nss, lane, BUFC);
 
     if (PP && pp) { // ping-pong: the two load buffers swap roles, no register copies
         for (;;) {
@@ -1257,7 +1269,12 @@ __device__ __forceinline__ uint4 pk_ld(uint64_t a) {
 // conditional: a lane that skipped one would keep its register's previous
 // value alive.  (CPU model of every address: tests/kernel_model.py
 // packed_row_crc, test_packed_loads_stay_in_bounds.)
-template <bool EDGE, bool NTL, int RW = 16>
+// TEL (with NTL): the lanes whose 16 bytes reach the 128-byte line holding
+// the superstep's last byte load it without the nontemporal hint, so the
+// line stays in L2 for the next superstep's first lanes (a record at any byte
+// offset shares one line per superstep boundary; TEL 2: also the line of the
+// row's first load, which the record before it shares)
+template <bool EDGE, bool NTL, int RW = 16, int TEL = 0>
 __device__ __forceinline__ void pk_load(uint64_t pb, int32_t kb, uint32_t fl, uint32_t s, uint32_t lane,
                                         uint4 (&buf)[K]) {
     using R = PkRow<RW>;
@@ -1273,7 +1290,19 @@ __device__ __forceinline__ void pk_load(uint64_t pb, int32_t kb, uint32_t fl, ui
             const int32_t k = (int32_t)(R::PPS * s + RW * i + (lane % RW)) - kb;
             a = k <= 0 ? F0 : a; // k == 0: F0 is piece 0 itself (or its safe block)
         }
-        buf[i] = pk_ld<NTL>(a);
+        if constexpr (NTL && TEL > 0) {
+            bool t = false;
+            if (i == K - 1)
+                t = ((a + 15) >> 7) == ((base + 16u * R::PPS - 1) >> 7);
+            if (TEL > 1 && i == 0)
+                t = s == 0 && (a >> 7) == (base >> 7);
+            if (t)
+                buf[i] = pk_ld<false>(a);
+            else
+                buf[i] = pk_ld<true>(a);
+        } else {
+            buf[i] = pk_ld<NTL>(a);
+        }
     }
 }
 
@@ -1379,7 +1408,7 @@ __device__ __forceinline__ uint64_t pk_first_record(const UnitPrefix &us, uint64
 // have landed (one superstep of loads in flight per wave); 0 = two
 
 template <int WGT, int WPE, int DYN = 4, int CPW = 4, uint32_t DYN_POOLS = 32, bool SP = true, int WAITP = 0,
-          bool NTL = true, bool VM = false, int RW = 16, bool SB = false>
+          bool NTL = true, bool VM = false, int RW = 16, bool SB = false, int TEL = 0>
 __global__ __launch_bounds__(WGT, WPE) void crc_packed_kernel(
     const uint8_t *__restrict__ arena, const uint64_t *__restrict__ offsets,
     const uint32_t *__restrict__ lengths, const PlanArgs plan, uint64_t n,
@@ -1523,9 +1552,9 @@ __global__ __launch_bounds__(WGT, WPE) void crc_packed_kernel(
             if (s == 0)
                 pk_meta<VM, RW>(m, offsets, lengths, p.r0 + NR, n, lane);
             if ((int32_t)(R::PPS * s) > p.kmax)
-                pk_load<false, NTL, RW>(g.pb, g.kb, g.fl, s, lane, buf);
+                pk_load<false, NTL, RW, TEL>(g.pb, g.kb, g.fl, s, lane, buf);
             else
-                pk_load<true, NTL, RW>(g.pb, g.kb, g.fl, s, lane, buf);
+                pk_load<true, NTL, RW, TEL>(g.pb, g.kb, g.fl, s, lane, buf);
         };
         issue(gc, pc, 0, cur);
         uint32_t css = 0, acc = 0;
@@ -1749,9 +1778,13 @@ const KernelVariant kVariants[] = {
     {"pk_wg1024_dyn4c4p32_sp_vm_sb", crc_packed_kernel<1024, 8, 4, 4, 32, true, 0, true, true, 16, true>, 1024, WG_PER_CU, UO_PK},
     {"pk8_wg1024_dyn4c4p32_sp_vm_sb", crc_packed_kernel<1024, 8, 4, 4, 32, true, 0, true, true, 8, true>, 1024, WG_PER_CU, UO_PK},
     {"pk4_wg1024_dyn4c4p32_sp_vm_sb", crc_packed_kernel<1024, 8, 4, 4, 32, true, 0, true, true, 4, true>, 1024, WG_PER_CU, UO_PK},
+    {"pk_wg1024_dyn4c4p32_sp_vm_sb_tel1", crc_packed_kernel<1024, 8, 4, 4, 32, true, 0, true, true, 16, true, 1>, 1024, WG_PER_CU, UO_PK},
+    {"pk_wg1024_dyn4c4p32_sp_vm_sb_tel2", crc_packed_kernel<1024, 8, 4, 4, 32, true, 0, true, true, 16, true, 2>, 1024, WG_PER_CU, UO_PK},
+    {"pk8_wg1024_dyn4c4p32_sp_vm_sb_tel1", crc_packed_kernel<1024, 8, 4, 4, 32, true, 0, true, true, 8, true, 1>, 1024, WG_PER_CU, UO_PK},
     // rows of 32 lanes (two records per wave)
     {"pk32_wg768_dyn4c4p32_sp_vm_sb", crc_packed_kernel<768, 6, 4, 4, 32, true, 0, true, true, 32, true>, 768, WG_PER_CU, UO_PK},
 
+    {"v3_wg768_nt_dyn4c4p32_sp_xp_tel1", crc_batch_kernel_v3<768, 6, false, 0, UNIT_OVH, false, true, false, 0, 4, 4, 32, true, 0, false, false, true, DWG_MIN_BYTES, false, false, 1>, 768},
 };
 constexpr int kNumVariants = (int)(sizeof(kVariants) / sizeof(kVariants[0]));
 std::atomic<int> g_variant{-1};
