@@ -1785,6 +1785,10 @@ const KernelVariant kVariants[] = {
     {"pk32_wg768_dyn4c4p32_sp_vm_sb", crc_packed_kernel<768, 6, 4, 4, 32, true, 0, true, true, 32, true>, 768, WG_PER_CU, UO_PK},
 
     {"v3_wg768_nt_dyn4c4p32_sp_xp_tel1", crc_batch_kernel_v3<768, 6, false, 0, UNIT_OVH, false, true, false, 0, 4, 4, 32, true, 0, false, false, true, DWG_MIN_BYTES, false, false, 1>, 768},
+    {"pk_wg1024_dyn6c4p32_sp_vm_sb", crc_packed_kernel<1024, 8, 6, 4, 32, true, 0, true, true, 16, true>, 1024, WG_PER_CU, UO_PK},
+    {"pk_wg1024_dyn4c2p32_sp_vm_sb", crc_packed_kernel<1024, 8, 4, 2, 32, true, 0, true, true, 16, true>, 1024, WG_PER_CU, UO_PK},
+    {"pk_wg1024_dyn2c4p32_sp_vm_sb", crc_packed_kernel<1024, 8, 2, 4, 32, true, 0, true, true, 16, true>, 1024, WG_PER_CU, UO_PK},
+    {"pk_wg1024_dyn4c4p8_sp_vm_sb", crc_packed_kernel<1024, 8, 4, 4, 8, true, 0, true, true, 16, true>, 1024, WG_PER_CU, UO_PK},
 };
 constexpr int kNumVariants = (int)(sizeof(kVariants) / sizeof(kVariants[0]));
 std::atomic<int> g_variant{-1};
