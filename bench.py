@@ -894,11 +894,13 @@ def main():
             # the output of the last timed step, at full size, against the reference
             p2 = workload_parity(other, out2, 0, args.gib)
             log(f"{other} parity: {p2}")
+            t2, t2_src = pmc_traffic(other)
             extra[other] = {"desc": d2, "records": len(l2), "gibs": round(pb * args.steps / (tb - ta) / GIB, 2),
                             "shape": "packed kernel, rows of 16 lanes (max_length 4096)" if ml else "default",
                             "parity": p2, "kernel_ms": round(km / max(kl, 1), 4),
                             "roofline_frac": round((pb + 16 * len(l2)) / (km / max(kl, 1) / 1e3) / 1e9
-                                                   / HBM_PEAK_GBS, 4)}
+                                                   / HBM_PEAK_GBS, 4),
+                            "traffic": t2, "traffic_source": t2_src}
             del a2, do2, dl2, out2
             torch.cuda.empty_cache()
 
