@@ -1789,6 +1789,7 @@ const KernelVariant kVariants[] = {
     {"pk_wg1024_dyn4c2p32_sp_vm_sb", crc_packed_kernel<1024, 8, 4, 2, 32, true, 0, true, true, 16, true>, 1024, WG_PER_CU, UO_PK},
     {"pk_wg1024_dyn2c4p32_sp_vm_sb", crc_packed_kernel<1024, 8, 2, 4, 32, true, 0, true, true, 16, true>, 1024, WG_PER_CU, UO_PK},
     {"pk_wg1024_dyn4c4p8_sp_vm_sb", crc_packed_kernel<1024, 8, 4, 4, 8, true, 0, true, true, 16, true>, 1024, WG_PER_CU, UO_PK},
+    {"v3_wg1024_nt_dyn4c4p32_sp_xp", crc_batch_kernel_v3<1024, 8, false, 0, UNIT_OVH, false, true, false, 0, 4, 4, 32, true, 0, false, false, true>, 1024},
 };
 constexpr int kNumVariants = (int)(sizeof(kVariants) / sizeof(kVariants[0]));
 std::atomic<int> g_variant{-1};
